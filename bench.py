@@ -1,0 +1,226 @@
+"""FIA influence-query throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ml1m-mf|yelp-ncf|20m-mf64]
+
+A step = one pass of the hot path over one batch: per-entity Hessian caches
+(fia_prepare), related-set counts + offsets (fia_count_related), and the
+batched query (fia_query_batch: exact solve, every related rating's influence
++ train row, top-1 influencer) over the workload's whole query set, all
+resident in HBM.  With N > 1 (torchrun, one rank per GPU) every rank runs the
+same per-GPU batch (weak scaling: the node answers N x the query set) and the
+step ends with the RCCL all_gather of the top-K influencer lists.
+
+Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (k_score:
+gather + scoring) by SURVEY.md 8d's algorithmic bytes over its HIP-event
+duration; `cpu_baseline` times the reference ALGORITHM (oracle/ncg_port.py:
+O(N) scans, fmin_ncg with the reference arguments, per-rating gradient loop)
+on a bounded sample on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fia-kdd-19_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+
+CONFIGS = {
+    "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m"),
+    "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp"),
+    "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
+                     k=64, data="20m"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="ml1m-mf", choices=sorted(CONFIGS))
+    ap.add_argument("--topk", type=int, default=1)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
+    return ap.parse_args()
+
+
+def load_data(cfg):
+    from influence import synth
+    if cfg["data"] == "ml1m":
+        d = synth.make_dataset(synth.ML1M, seed=0)
+    elif cfg["data"] == "yelp":
+        d = synth.make_dataset(synth.YELP, seed=0)
+    else:
+        d = synth.make_20m(seed=0)
+    k = cfg["k"]
+    params = (synth.mf_params if cfg["model"] == "MF" else synth.ncf_params)(d["U"], d["I"], k, 0)
+    return d, params
+
+
+def bytes_per_query(model, k, n):
+    """SURVEY.md 8d algorithmic bytes per query: MF n(4k+32) + 8k+8; NCF n(8k+32)."""
+    n = np.asarray(n, np.float64)
+    if model == "MF":
+        return n * (4 * k + 32) + 8 * k + 8
+    return n * (8 * k + 32)
+
+
+def cpu_baseline(cfg, d, params, seconds):
+    """Reference algorithm on the host (1 BLAS thread), RQ1 query order, time-bounded."""
+    from oracle import ncg_port
+    from influence import synth
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:
+        lim = None
+    tu, ti, tr = d["train"]
+    qu, qi, _ = d["test"]
+    port = ncg_port.RefAlgorithm(cfg["model"], params, cfg["k"], tu, ti, tr, 1e-3, 1e-6)
+    order = synth.rq1_query_indices(min(100, qu.size), qu.size) if cfg["data"] == "ml1m" else \
+        np.random.default_rng(0).choice(qu.size, min(100, qu.size), replace=False)
+    t0 = time.time()
+    done = 0
+    for t in order:
+        port.get_influence_on_test_loss(int(qu[t]), int(qi[t]))
+        done += 1
+        if time.time() - t0 > seconds and done >= 3:
+            break
+    dt = time.time() - t0
+    if lim is not None:
+        lim.unregister() if hasattr(lim, "unregister") else None
+    return dict(value=done / dt, unit="queries/s", cores=1, kind="port",
+                sample="%d %s queries in %.1f s (reference algorithm: np.where scans + scipy fmin_ncg "
+                       "avextol=1e-3 maxiter=100 with the verbose callback + per-rating gradient loop)"
+                       % (done, "RQ1-order" if cfg["data"] == "ml1m" else "random", dt))
+
+
+def main():
+    args = parse()
+    cfg = CONFIGS[args.config]
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from influence import _lib
+    from influence.sharding import gather_topk
+
+    d, params = load_data(cfg)
+    tu, ti, tr = d["train"]
+    qu_np, qi_np, _ = d["test"]
+    if world > 1 and rank > 0:       # same per-GPU batch, rank-rotated order
+        shift = (rank * qu_np.size) // world
+        qu_np, qi_np = np.roll(qu_np, -shift), np.roll(qi_np, -shift)
+    Q = int(qu_np.size)
+    U, I, k = d["U"], d["I"], cfg["k"]
+    model_id = _lib.FIA_MODEL_MF if cfg["model"] == "MF" else _lib.FIA_MODEL_NCF
+
+    ctx = _lib.Context(local)
+    names = list(params)
+    tables = [torch.from_numpy(np.ascontiguousarray(params[n], np.float32)).to(dev) for n in names]
+    ctx.set_params(model_id, k, U, I, tables, 1e-3, 1e-6)
+    t_u = torch.from_numpy(tu).to(dev)
+    t_i = torch.from_numpy(ti).to(dev)
+    t_r = torch.from_numpy(tr).to(dev)
+    t0 = time.time()
+    ctx.build_index(t_u, t_i, t_r, U, I)
+    torch.cuda.synchronize(dev)
+    index_s = time.time() - t0
+    qu = torch.from_numpy(qu_np).to(dev)
+    qi = torch.from_numpy(qi_np).to(dev)
+    offsets, total = ctx.count_related(qu, qi)
+    n_q = np.diff(offsets.cpu().numpy())
+    D = ctx.num_params()
+    K = args.topk
+    rel = torch.empty(total, dtype=torch.int64, device=dev)
+    infl = torch.empty(total, dtype=torch.float64, device=dev)
+    xbuf = torch.empty(Q * D, dtype=torch.float64, device=dev)
+    tp = torch.empty(Q * K, dtype=torch.int64, device=dev)
+    tix = torch.empty(Q * K, dtype=torch.int64, device=dev)
+    tv = torch.empty(Q * K, dtype=torch.float64, device=dev)
+
+    def step():
+        ctx.prepare()
+        ctx.count_related(qu, qi, offsets, want_total=False)
+        ctx.query_batch(qu, qi, offsets, total, rel, infl, xbuf, K, tp, tix, tv)
+        if world > 1:
+            gather_topk(tix.view(Q, K), tv.view(Q, K))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.profile_read()
+    ctx.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_profiling(False)
+    phases = ctx.profile_read()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * Q * args.steps / elapsed
+    score_ms = phases["score"][0] / max(phases["score"][1], 1)
+    bytes_launch = float(bytes_per_query(cfg["model"], k, n_q).sum())
+    achieved = bytes_launch / (score_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "influence queries/sec (whole node) + % HBM roofline, MF k=16 ML-1M-ex"
+        if args.config == "ml1m-mf" else "influence queries/sec (whole node), " + cfg["workload"],
+        "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic train ratings of the reference shape (train file not distributed) + the reference's "
+                "real held-out test pairs; synthetic parameters",
+        "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_gpu": Q,
+                   "n_train": int(tu.size), "related_ratings_per_gpu_step": int(total), "topk": K,
+                   "parallelism": "dp%d (query shards, top-K all_gather)" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_score", "kernel_ms": score_ms, "algorithmic_bytes_per_launch": bytes_launch},
+        "phases_ms_per_step": {p: (v[0] / max(v[1], 1)) for p, v in phases.items()},
+        "index_build_s": index_s,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, d, params, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,288 @@
+// C ABI entry points (include/fia.h).  Validates arguments, keeps the context
+// state machine (params -> index -> prepare -> query), converts HIP errors to
+// status codes + a message, and never lets an exception cross the boundary.
+#include <cstring>
+#include <new>
+
+#include "common.h"
+
+namespace fia {
+
+static bool pooled_event(fia_ctx* c, hipEvent_t* e) {
+  if (!c->events.pool.empty()) {
+    *e = c->events.pool.back();
+    c->events.pool.pop_back();
+    return true;
+  }
+  return hipEventCreate(e) == hipSuccess;
+}
+
+void phase_begin(fia_ctx* c, int phase, hipStream_t s) {
+  if (!c->profiling) return;
+  hipEvent_t a, b;
+  if (!pooled_event(c, &a)) return;
+  if (!pooled_event(c, &b)) { c->events.pool.push_back(a); return; }
+  (void)hipEventRecord(a, s);
+  c->events.ev[phase].push_back({a, b});
+}
+
+void phase_end(fia_ctx* c, int phase, hipStream_t s) {
+  if (!c->profiling || c->events.ev[phase].empty()) return;
+  (void)hipEventRecord(c->events.ev[phase].back().second, s);
+}
+
+}  // namespace fia
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int fail(fia_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+int hip_fail(fia_ctx* c, hipError_t e, const char* where) {
+  return fail(c, FIA_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define FIA_GUARDED(ctx, ...)                                          \
+  try {                                                                \
+    __VA_ARGS__                                                        \
+  } catch (const std::bad_alloc&) {                                    \
+    return fail(ctx, FIA_ERR_NOMEM, "host allocation failed");         \
+  } catch (...) {                                                      \
+    return fail(ctx, FIA_ERR_INVALID, "unexpected internal exception"); \
+  }
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+int fia_version(void) { return 100; }
+
+int fia_create(int device, fia_ctx** out) {
+  if (!out) return FIA_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return FIA_ERR_HIP;
+  if (device < 0 || device >= n) return FIA_ERR_INVALID;
+  fia_ctx* c = new (std::nothrow) fia_ctx();
+  if (!c) return FIA_ERR_NOMEM;
+  c->device = device;
+  *out = c;
+  return FIA_OK;
+}
+
+int fia_destroy(fia_ctx* c) {
+  if (!c) return FIA_OK;
+  {
+    DeviceGuard g(c->device);
+    (void)hipDeviceSynchronize();
+    for (int s = 0; s < 2; ++s) {
+      c->idx.side[s].ptr.release();
+      c->idx.side[s].row.release();
+      c->idx.side[s].other.release();
+      c->idx.side[s].rating.release();
+      c->gram[s].release();
+      c->l1[s].release();
+    }
+    fia::DevBuf* bufs[] = {&c->rec, &c->coff, &c->cquery, &c->cstart, &c->cand_pos,
+                           &c->cand_val, &c->scan_tmp, &c->flag, &c->nch};
+    for (auto* b : bufs) b->release();
+    for (auto& v : c->events.ev)
+      for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto e : c->events.pool) (void)hipEventDestroy(e);
+  }
+  delete c;
+  return FIA_OK;
+}
+
+const char* fia_last_error(const fia_ctx* c) { return c ? c->err.c_str() : ""; }
+
+int fia_num_params(const fia_ctx* c) {
+  if (!c || !c->p.valid) return 0;
+  return fia::model_num_params(c->p.model, c->p.k);
+}
+
+int fia_set_params(fia_ctx* c, int model, int k, int64_t U, int64_t I, const float* const* tables, int nptrs,
+                   double wd, double damping) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (model != FIA_MODEL_MF && model != FIA_MODEL_NCF) return fail(c, FIA_ERR_INVALID, "unknown model");
+    const int need = model == FIA_MODEL_MF ? 5 : 10;
+    if (!tables || nptrs != need) return fail(c, FIA_ERR_INVALID, "wrong number of parameter tables");
+    for (int t = 0; t < need; ++t)
+      if (!tables[t]) return fail(c, FIA_ERR_INVALID, "null parameter table");
+    if (U <= 0 || I <= 0 || U >= (1LL << 31) || I >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "bad table sizes");
+    if (!fia::model_supported(model, k))
+      return fail(c, FIA_ERR_UNSUPPORTED, "embedding size " + std::to_string(k) + " not built for this model");
+    if (!(wd >= 0.0) || !(damping >= 0.0)) return fail(c, FIA_ERR_INVALID, "weight_decay/damping must be >= 0");
+    if (c->idx.valid && (c->idx.U != U || c->idx.I != I))
+      return fail(c, FIA_ERR_INVALID, "num_users/num_items differ from the built index");
+    c->p.model = model;
+    c->p.k = k;
+    c->p.U = U;
+    c->p.I = I;
+    for (int t = 0; t < 10; ++t) c->p.t[t] = t < need ? tables[t] : nullptr;
+    c->p.wd = wd;
+    c->p.damping = damping;
+    c->p.valid = true;
+    c->prepared = false;
+    return FIA_OK;
+  })
+}
+
+int fia_build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* user, const int32_t* item,
+                    const float* rating, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (N < 0 || N >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "n_train out of range");
+    if (U <= 0 || I <= 0 || U >= (1LL << 31) || I >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "bad entity counts");
+    if (N > 0 && (!user || !item || !rating)) return fail(c, FIA_ERR_INVALID, "null training array");
+    if (c->p.valid && (c->p.U != U || c->p.I != I))
+      return fail(c, FIA_ERR_INVALID, "num_users/num_items differ from the registered params");
+    DeviceGuard g(c->device);
+    std::string why;
+    hipError_t e = fia::build_index(c, N, U, I, user, item, rating, as_stream(stream), why);
+    c->prepared = false;
+    if (e != hipSuccess) {
+      if (!why.empty()) return fail(c, FIA_ERR_INVALID, why);
+      return hip_fail(c, e, "fia_build_index");
+    }
+    return FIA_OK;
+  })
+}
+
+int fia_prepare(fia_ctx* c, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (!c->p.valid) return fail(c, FIA_ERR_STATE, "fia_set_params has not been called");
+    if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
+    DeviceGuard g(c->device);
+    hipStream_t s = as_stream(stream);
+    bool unsup = false;
+    fia::phase_begin(c, 0, s);
+    hipError_t e = fia::prepare_model(c, s, unsup);
+    fia::phase_end(c, 0, s);
+    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
+    if (e != hipSuccess) return hip_fail(c, e, "fia_prepare");
+    c->prepared = true;
+    return FIA_OK;
+  })
+}
+
+int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* offsets,
+                      int64_t* total_out, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
+    if (Q < 0 || Q >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "num_queries out of range");
+    if (!offsets || (Q > 0 && (!qu || !qi))) return fail(c, FIA_ERR_INVALID, "null query array");
+    DeviceGuard g(c->device);
+    hipStream_t s = as_stream(stream);
+    hipError_t e;
+    if (total_out) {
+      e = c->flag.reserve(64);
+      if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
+      e = hipMemsetAsync(c->flag.ptr, 0, 64, s);
+      if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
+    }
+    e = fia::count_related(c, Q, qu, qi, offsets, s);
+    if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
+    if (total_out) {
+      int32_t flags[4] = {0, 0, 0, 0};
+      e = hipMemcpyAsync(total_out, offsets + Q, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(flags, c->flag.ptr, sizeof(flags), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
+      if (flags[1]) return fail(c, FIA_ERR_INVALID, "query ids out of range [0, num_users) x [0, num_items)");
+    }
+    return FIA_OK;
+  })
+}
+
+int fia_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                int64_t* rel_idx, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
+    if (Q < 0 || Q >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "num_queries out of range");
+    if (Q > 0 && (!qu || !qi || !offsets || !rel_idx)) return fail(c, FIA_ERR_INVALID, "null array");
+    DeviceGuard g(c->device);
+    hipError_t e = fia::write_related(c, Q, qu, qi, offsets, rel_idx, as_stream(stream));
+    if (e != hipSuccess) return hip_fail(c, e, "fia_related");
+    return FIA_OK;
+  })
+}
+
+int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                    int64_t total_rel, int64_t* rel_idx, double* influence, double* x_out, int K,
+                    int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (!c->p.valid || !c->idx.valid) return fail(c, FIA_ERR_STATE, "params/index missing");
+    if (!c->prepared) return fail(c, FIA_ERR_STATE, "fia_prepare has not been called since params/index changed");
+    if (Q < 0 || Q >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "num_queries out of range");
+    if (total_rel < 0) return fail(c, FIA_ERR_INVALID, "total_rel < 0");
+    if (K < 0 || K > FIA_MAX_TOPK) return fail(c, FIA_ERR_INVALID, "K must be in [0, FIA_MAX_TOPK]");
+    if (Q > 0 && (!qu || !qi || !offsets)) return fail(c, FIA_ERR_INVALID, "null query array");
+    if (K > 0 && (!topk_pos || !topk_idx || !topk_val)) return fail(c, FIA_ERR_INVALID, "null top-K output");
+    if (Q == 0) return FIA_OK;
+    DeviceGuard g(c->device);
+    const int64_t max_chunks = Q + total_rel / fia::kChunk + 1;
+    bool unsup = false;
+    hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,
+                                    topk_idx, topk_val, as_stream(stream), unsup);
+    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
+    if (e != hipSuccess) return hip_fail(c, e, "fia_query_batch");
+    return FIA_OK;
+  })
+}
+
+int fia_set_profiling(fia_ctx* c, int enable) {
+  if (!c) return FIA_ERR_INVALID;
+  c->profiling = enable != 0;
+  return FIA_OK;
+}
+
+int fia_profile_read(fia_ctx* c, double* ms_sum, int64_t* counts) {
+  if (!c || !ms_sum || !counts) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    DeviceGuard g(c->device);
+    int rc = FIA_OK;
+    for (int ph = 0; ph < FIA_NUM_PHASES; ++ph) {
+      double sum = 0.0;
+      int64_t cnt = 0;
+      for (auto& pr : c->events.ev[ph]) {
+        float ms = 0.f;
+        if (hipEventSynchronize(pr.second) == hipSuccess && hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+          sum += ms;
+          ++cnt;
+        } else {
+          rc = fail(c, FIA_ERR_HIP, "event timing failed");
+        }
+        c->events.pool.push_back(pr.first);
+        c->events.pool.push_back(pr.second);
+      }
+      c->events.ev[ph].clear();
+      ms_sum[ph] = sum;
+      counts[ph] = cnt;
+    }
+    return rc;
+  })
+}
+
+}  // extern "C"

@@ -1,0 +1,223 @@
+// Rating index (CSR by user, CSC by item), related-set counting and the
+// per-batch chunk list.
+//
+// Replaces the reference's per-query O(N) scans
+//   u_indices = np.where(train.x[:, 0] == test_u)   (matrix_factorization.py:320)
+//   i_indices = np.where(train.x[:, 1] == test_i)   (matrix_factorization.py:321)
+// with a one-time stable radix sort: inside every list train rows stay in
+// ascending order, so rel(u,i) = R_u ++ C_i is the reference's concatenation
+// bit for bit (mf:322).
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include "common.h"
+
+namespace fia {
+namespace {
+
+__global__ void k_check_ids(const int32_t* __restrict__ user, const int32_t* __restrict__ item, int64_t N,
+                            int64_t U, int64_t I, int32_t* __restrict__ flag) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int bad = 0;
+  for (; j < N; j += stride) {
+    int32_t u = user[j], i = item[j];
+    bad |= (u < 0 || u >= U || i < 0 || i >= I);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+__global__ void k_gather_side(const int32_t* __restrict__ rows, const int32_t* __restrict__ other_src,
+                              const float* __restrict__ rating_src, int64_t N, int32_t* __restrict__ other,
+                              float* __restrict__ rating) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; j < N; j += stride) {
+    int32_t r = rows[j];
+    other[j] = other_src[r];
+    rating[j] = rating_src[r];
+  }
+}
+
+// ptr[e] = lower_bound(sorted_keys, e), e in [0, n_entity]
+__global__ void k_list_ptr(const int32_t* __restrict__ keys, int64_t N, int64_t n_entity, int64_t* __restrict__ ptr) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e > n_entity) return;
+  int64_t lo = 0, hi = N;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < e) lo = mid + 1; else hi = mid;
+  }
+  ptr[e] = lo;
+}
+
+__global__ void k_count(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
+                        const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
+                        int64_t* __restrict__ counts, int32_t* __restrict__ flag) {
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > Q) return;
+  if (q == Q) { counts[Q] = 0; return; }
+  int32_t u = qu[q], i = qi[q];
+  int64_t n = 0;
+  bool ok = (u >= 0 && u < U && i >= 0 && i < I);
+  if (ok) n = (uptr[u + 1] - uptr[u]) + (iptr[i + 1] - iptr[i]);
+  else atomicOr(flag + 1, 1);
+  counts[q] = n;
+}
+
+__global__ void k_chunk_counts(const int64_t* __restrict__ offsets, int64_t Q, int64_t* __restrict__ nch) {
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > Q) return;
+  if (q == Q) { nch[Q] = 0; return; }
+  int64_t n = offsets[q + 1] - offsets[q];
+  nch[q] = (n + kChunk - 1) / kChunk;
+}
+
+__global__ void k_chunk_fill(const int64_t* __restrict__ coff, int64_t Q, int32_t* __restrict__ cquery,
+                             int32_t* __restrict__ cstart) {
+  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  int64_t b = coff[q], e = coff[q + 1];
+  for (int64_t c = b; c < e; ++c) {
+    cquery[c] = (int32_t)q;
+    cstart[c] = (int32_t)((c - b) * kChunk);
+  }
+}
+
+// one workgroup per query: rel[offsets[q] + p] = R_u[p] (p < deg u), then C_i
+__global__ void k_write_related(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi,
+                                const int64_t* __restrict__ offsets, const int64_t* __restrict__ uptr,
+                                const int32_t* __restrict__ urow, const int64_t* __restrict__ iptr,
+                                const int32_t* __restrict__ irow, int64_t U, int64_t I, int64_t* __restrict__ rel) {
+  int64_t q = blockIdx.x;
+  int32_t u = qu[q], i = qi[q];
+  if (u < 0 || u >= U || i < 0 || i >= I) return;
+  int64_t base = offsets[q];
+  int64_t ub = uptr[u], du = uptr[u + 1] - ub;
+  int64_t ib = iptr[i], di = iptr[i + 1] - ib;
+  for (int64_t p = threadIdx.x; p < du; p += blockDim.x) rel[base + p] = urow[ub + p];
+  for (int64_t p = threadIdx.x; p < di; p += blockDim.x) rel[base + du + p] = irow[ib + p];
+}
+
+inline unsigned bits_for(int64_t n) {
+  unsigned b = 1;
+  while (b < 31 && ((int64_t)1 << b) < n) ++b;
+  return b;
+}
+
+inline int grid_for(int64_t n, int threads, int cap = 8192) {
+  int64_t g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace
+
+hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s) {
+  size_t tb = 0;
+  FIA_HIP_TRY(rocprim::exclusive_scan(nullptr, tb, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), s));
+  FIA_HIP_TRY(c->scan_tmp.reserve(tb + 16));
+  size_t tb2 = c->scan_tmp.bytes;
+  return rocprim::exclusive_scan(c->scan_tmp.ptr, tb2, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), s);
+}
+
+hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* user, const int32_t* item,
+                       const float* rating, hipStream_t s, std::string& why) {
+  Index& X = c->idx;
+  X.valid = false;
+  FIA_HIP_TRY(c->flag.reserve(64));
+  FIA_HIP_TRY(hipMemsetAsync(c->flag.ptr, 0, 64, s));
+  if (N > 0) {
+    hipLaunchKernelGGL(k_check_ids, dim3(grid_for(N, 256)), dim3(256), 0, s, user, item, N, U, I,
+                       c->flag.as<int32_t>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  int32_t hflag = 0;
+  FIA_HIP_TRY(hipMemcpyAsync(&hflag, c->flag.ptr, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  FIA_HIP_TRY(hipStreamSynchronize(s));
+  if (hflag) {
+    why = "training ids out of range [0, num_users) x [0, num_items)";
+    return hipErrorInvalidValue;
+  }
+  DevBuf keys_sorted, tmp;
+  FIA_HIP_TRY(keys_sorted.reserve(sizeof(int32_t) * (size_t)(N > 0 ? N : 1)));
+  const int32_t* key_src[2] = {user, item};
+  const int32_t* other_src[2] = {item, user};
+  int64_t n_ent[2] = {U, I};
+  for (int sd = 0; sd < 2; ++sd) {
+    Side& S = X.side[sd];
+    size_t nb = sizeof(int32_t) * (size_t)(N > 0 ? N : 1);
+    FIA_HIP_TRY(S.row.reserve(nb));
+    FIA_HIP_TRY(S.other.reserve(nb));
+    FIA_HIP_TRY(S.rating.reserve(sizeof(float) * (size_t)(N > 0 ? N : 1)));
+    FIA_HIP_TRY(S.ptr.reserve(sizeof(int64_t) * (size_t)(n_ent[sd] + 1)));
+    if (N > 0) {
+      unsigned eb = bits_for(n_ent[sd]);
+      rocprim::counting_iterator<int32_t> iota(0);
+      size_t tb = 0;
+      FIA_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, key_src[sd], keys_sorted.as<int32_t>(), iota,
+                                            S.row.as<int32_t>(), (size_t)N, 0u, eb, s));
+      FIA_HIP_TRY(tmp.reserve(tb + 16));
+      tb = tmp.bytes;
+      FIA_HIP_TRY(rocprim::radix_sort_pairs(tmp.ptr, tb, key_src[sd], keys_sorted.as<int32_t>(), iota,
+                                            S.row.as<int32_t>(), (size_t)N, 0u, eb, s));
+      hipLaunchKernelGGL(k_gather_side, dim3(grid_for(N, 256)), dim3(256), 0, s, S.row.as<int32_t>(),
+                         other_src[sd], rating, N, S.other.as<int32_t>(), S.rating.as<float>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_list_ptr, dim3((unsigned)((n_ent[sd] + 1 + 255) / 256)), dim3(256), 0, s,
+                       keys_sorted.as<int32_t>(), N, n_ent[sd], S.ptr.as<int64_t>());
+    FIA_HIP_TRY(hipGetLastError());
+    FIA_HIP_TRY(hipStreamSynchronize(s));   // keys_sorted is reused by the next side
+  }
+  keys_sorted.release();
+  tmp.release();
+  X.N = N;
+  X.U = U;
+  X.I = I;
+  X.valid = true;
+  return hipSuccess;
+}
+
+hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* offsets,
+                         hipStream_t s) {
+  // counts go to the chunk-offset scratch, then an exclusive scan into offsets
+  FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
+  FIA_HIP_TRY(c->flag.reserve(64));
+  hipLaunchKernelGGL(k_count, dim3((unsigned)((Q + 1 + 255) / 256)), dim3(256), 0, s, qu, qi, Q,
+                     c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I,
+                     c->coff.as<int64_t>(), c->flag.as<int32_t>());
+  FIA_HIP_TRY(hipGetLastError());
+  return exclusive_scan_i64(c, c->coff.as<int64_t>(), offsets, Q + 1, s);
+}
+
+hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                         int64_t* rel, hipStream_t s) {
+  if (Q == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_write_related, dim3((unsigned)Q), dim3(256), 0, s, qu, qi, offsets,
+                     c->idx.side[0].ptr.as<int64_t>(), c->idx.side[0].row.as<int32_t>(),
+                     c->idx.side[1].ptr.as<int64_t>(), c->idx.side[1].row.as<int32_t>(), c->idx.U, c->idx.I, rel);
+  return hipGetLastError();
+}
+
+hipError_t build_chunks(fia_ctx* c, int64_t Q, const int64_t* offsets, int64_t max_chunks, hipStream_t s) {
+  FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
+  FIA_HIP_TRY(c->cquery.reserve(sizeof(int32_t) * (size_t)(max_chunks + 1)));
+  FIA_HIP_TRY(c->cstart.reserve(sizeof(int32_t) * (size_t)(max_chunks + 1)));
+  FIA_HIP_TRY(c->nch.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
+  int64_t* nch = c->nch.as<int64_t>();
+  hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)((Q + 1 + 255) / 256)), dim3(256), 0, s, offsets, Q, nch);
+  FIA_HIP_TRY(hipGetLastError());
+  FIA_HIP_TRY(exclusive_scan_i64(c, nch, c->coff.as<int64_t>(), Q + 1, s));
+  if (Q > 0) {
+    hipLaunchKernelGGL(k_chunk_fill, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, c->coff.as<int64_t>(), Q,
+                       c->cquery.as<int32_t>(), c->cstart.as<int32_t>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+}  // namespace fia

@@ -1,0 +1,162 @@
+"""ctypes binding of libfia.so (include/fia.h) for torch device tensors.
+
+This is the ONLY compute path of the package: there is no CPU fallback.  If
+the library is missing (not built) or no GPU is visible, every entry point
+raises, loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FIA_LIB", os.path.join(_HERE, "libfia.so"))
+
+FIA_OK = 0
+FIA_MODEL_MF = 0
+FIA_MODEL_NCF = 1
+FIA_MAX_TOPK = 64
+FIA_NUM_PHASES = 5
+PHASES = ("prepare", "solve", "score", "topk", "chunks")
+
+_ERR = {1: "invalid argument", 2: "HIP error", 3: "bad call order", 4: "unsupported", 5: "out of memory"}
+
+# exported symbol -> (restype, argtypes); every symbol declared in include/fia.h
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+SIGNATURES = {
+    "fia_version": (ctypes.c_int, []),
+    "fia_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    "fia_destroy": (ctypes.c_int, [_P]),
+    "fia_last_error": (ctypes.c_char_p, [_P]),
+    "fia_set_params": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _I64, _I64, ctypes.POINTER(_P), ctypes.c_int,
+                                      ctypes.c_double, ctypes.c_double]),
+    "fia_build_index": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _P, _P, _P]),
+    "fia_prepare": (ctypes.c_int, [_P, _P]),
+    "fia_count_related": (ctypes.c_int, [_P, _I64, _P, _P, _P, ctypes.POINTER(_I64), _P]),
+    "fia_related": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
+    "fia_query_batch": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P]),
+    "fia_num_params": (ctypes.c_int, [_P]),
+    "fia_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
+    "fia_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)]),
+}
+
+_lib = None
+
+
+class FIAError(RuntimeError):
+    pass
+
+
+def load_library(path=None):
+    """dlopen libfia.so and bind every symbol (no GPU needed for this step)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError("FIA HIP library not built: %s is missing (run __graft_entry__.build() or "
+                          "make -C fia-kdd-19_amd/csrc)" % p)
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Context(object):
+    """One fia_ctx bound to one HIP device."""
+
+    def __init__(self, device=0):
+        import torch
+        if not torch.cuda.is_available():
+            raise FIAError("FIA needs a ROCm GPU: torch.cuda.is_available() is False (no CPU fallback)")
+        self.lib = load_library()
+        self.device = device
+        self.torch_device = torch.device("cuda", device)
+        h = ctypes.c_void_p()
+        rc = self.lib.fia_create(device, ctypes.byref(h))
+        if rc != FIA_OK:
+            raise FIAError("fia_create(%d) failed: %s" % (device, _ERR.get(rc, rc)))
+        self.h = h
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fia_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != FIA_OK:
+            msg = self.lib.fia_last_error(self.h)
+            raise FIAError("%s failed (%s): %s" % (what, _ERR.get(rc, rc), msg.decode() if msg else ""))
+
+    # ---- setup ----
+    def set_params(self, model, k, U, I, tables, wd, damping):
+        """tables: list of contiguous float32 cuda tensors in include/fia.h order."""
+        arr = (ctypes.c_void_p * len(tables))(*[t.data_ptr() for t in tables])
+        self._keep = list(tables)
+        rc = self.lib.fia_set_params(self.h, model, k, U, I, arr, len(tables), float(wd), float(damping))
+        self._check(rc, "fia_set_params")
+
+    def build_index(self, users, items, ratings, U, I):
+        rc = self.lib.fia_build_index(self.h, users.numel(), U, I, _ptr(users), _ptr(items), _ptr(ratings),
+                                      _stream())
+        self._check(rc, "fia_build_index")
+
+    def prepare(self):
+        self._check(self.lib.fia_prepare(self.h, _stream()), "fia_prepare")
+
+    def num_params(self):
+        return self.lib.fia_num_params(self.h)
+
+    # ---- queries ----
+    def count_related(self, qu, qi, offsets=None, want_total=True):
+        import torch
+        Q = qu.numel()
+        if offsets is None:
+            offsets = torch.empty(Q + 1, dtype=torch.int64, device=self.torch_device)
+        total = ctypes.c_int64(0)
+        rc = self.lib.fia_count_related(self.h, Q, _ptr(qu), _ptr(qi), _ptr(offsets),
+                                        ctypes.byref(total) if want_total else None, _stream())
+        self._check(rc, "fia_count_related")
+        return offsets, (total.value if want_total else None)
+
+    def related(self, qu, qi, offsets, rel_idx):
+        rc = self.lib.fia_related(self.h, qu.numel(), _ptr(qu), _ptr(qi), _ptr(offsets), _ptr(rel_idx), _stream())
+        self._check(rc, "fia_related")
+
+    def query_batch(self, qu, qi, offsets, total, rel_idx=None, influence=None, x=None, K=0,
+                    topk_pos=None, topk_idx=None, topk_val=None):
+        rc = self.lib.fia_query_batch(self.h, qu.numel(), _ptr(qu), _ptr(qi), _ptr(offsets), int(total),
+                                      _ptr(rel_idx), _ptr(influence), _ptr(x), int(K), _ptr(topk_pos),
+                                      _ptr(topk_idx), _ptr(topk_val), _stream())
+        self._check(rc, "fia_query_batch")
+
+    # ---- profiling ----
+    def set_profiling(self, on):
+        self._check(self.lib.fia_set_profiling(self.h, 1 if on else 0), "fia_set_profiling")
+
+    def profile_read(self):
+        ms = (ctypes.c_double * FIA_NUM_PHASES)()
+        cnt = (ctypes.c_int64 * FIA_NUM_PHASES)()
+        self._check(self.lib.fia_profile_read(self.h, ms, cnt), "fia_profile_read")
+        return {PHASES[p]: (ms[p], cnt[p]) for p in range(FIA_NUM_PHASES)}

@@ -1,0 +1,202 @@
+"""GPU parity of the HIP path (through the C ABI, via the reference-shaped
+facade) against the fp64 oracle's golden fixtures and, at full size, against
+size-independent properties.
+
+Tolerances (north star): related sets and top-K ordering bit-exact; influence
+and x within 1e-5 relative, normalised by the query's max |influence| / |x|
+(the kernels compute in fp64, so the observed error is ~1e-13)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from influence import synth
+from influence.dataset import DataSet
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def load(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def params_of(f):
+    return {k[3:].replace("__", "/"): f[k] for k in f if k.startswith("p__")}
+
+
+def make_model(model, U, I, k, train, test_pairs, params, wd=1e-3, damping=1e-6, tmpdir="output"):
+    from influence.matrix_factorization import MF
+    from influence.NCF import NCF
+    tu, ti, tr = train
+    qu, qi = test_pairs
+    data_sets = {"train": DataSet(np.stack([tu, ti], 1), np.asarray(tr, np.float64)),
+                 "validation": None,
+                 "test": DataSet(np.stack([qu, qi], 1), np.zeros(len(qu)))}
+    cls = MF if model == "MF" else NCF
+    return cls(num_users=int(U), num_items=int(I), embedding_size=int(k), weight_decay=wd, num_classes=1,
+               batch_size=3020, data_sets=data_sets, initial_learning_rate=1e-3, damping=damping,
+               decay_epochs=[10000, 20000], mini_batch=True, train_dir=str(tmpdir), log_dir="log",
+               avextol=1e-3, model_name="test_%s" % model, params=params, verbose=False)
+
+
+def rel_err(a, b):
+    s = np.abs(b).max(initial=0.0)
+    return np.abs(a - b).max(initial=0.0) / (s if s > 0 else 1.0)
+
+
+@pytest.mark.parametrize("name", ["small_mf_k16.npz", "small_ncf_k16.npz", "small_mf_k8.npz", "small_ncf_k8.npz"])
+def test_small_golden_single_query_api(name, tmp_path):
+    f = load(name)
+    model = "MF" if "_mf_" in name else "NCF"
+    m = make_model(model, f["U"], f["I"], f["k"], (f["train_user"], f["train_item"], f["train_rating"]),
+                   (f["q_user"], f["q_item"]), params_of(f), tmpdir=tmp_path)
+    N = f["train_user"].size
+    for q in range(f["q_user"].size):
+        b, e = f["offsets"][q], f["offsets"][q + 1]
+        rel = m.get_train_indices_of_test_case([q])
+        assert rel.dtype == np.int64 and np.array_equal(rel, f["rel"][b:e])
+        infl = m.get_influence_on_test_loss([q], np.arange(N))
+        assert np.array_equal(m.train_indices_of_test_case, f["rel"][b:e])
+        assert infl.dtype == np.float64 and infl.shape == (e - b,)
+        if e > b:
+            assert rel_err(infl, f["influence"][b:e]) < RTOL
+            assert rel_err(np.concatenate(m.inverse_hvp), f["x"][q]) < RTOL
+        else:
+            assert np.isnan(np.concatenate(m.inverse_hvp)).all()
+
+
+@pytest.mark.parametrize("name", ["small_mf_k16.npz", "small_ncf_k16.npz"])
+@pytest.mark.parametrize("K", [1, 3, 5, 64])
+def test_small_golden_batch_and_topk(name, K, tmp_path):
+    from oracle import fia_oracle as fo
+    f = load(name)
+    model = "MF" if "_mf_" in name else "NCF"
+    m = make_model(model, f["U"], f["I"], f["k"], (f["train_user"], f["train_item"], f["train_rating"]),
+                   (f["q_user"], f["q_item"]), params_of(f), tmpdir=tmp_path)
+    Q = f["q_user"].size
+    res = m.get_influence_batch(list(range(Q)), K=K)
+    assert np.array_equal(res["offsets"], f["offsets"])
+    assert np.array_equal(res["rel_idx"], f["rel"])
+    for q in range(Q):
+        b, e = f["offsets"][q], f["offsets"][q + 1]
+        if e > b:
+            assert rel_err(res["influence"][b:e], f["influence"][b:e]) < RTOL
+        want = fo.topk(f["influence"][b:e], K)
+        got = res["topk_pos"][q]
+        assert np.array_equal(got[:want.size], want)
+        assert (got[want.size:] == -1).all() and np.isnan(res["topk_val"][q][want.size:]).all()
+        assert np.array_equal(res["topk_idx"][q][:want.size], f["rel"][b:e][want])
+        np.testing.assert_array_equal(res["topk_val"][q][:want.size], res["influence"][b:e][want])
+
+
+def test_duplicate_rows_tie_by_position(tmp_path):
+    """The test pair present twice in train appears 4 times in rel with equal
+    influence per copy: top-K must list equal values by related position."""
+    f = load("small_mf_k16.npz")
+    m = make_model("MF", f["U"], f["I"], f["k"], (f["train_user"], f["train_item"], f["train_rating"]),
+                   (f["q_user"], f["q_item"]), params_of(f), tmpdir=tmp_path)
+    q = 2   # (tu[7], ti[7]) duplicated in train
+    res = m.get_influence_batch([q], K=8)
+    infl = res["influence"]
+    order = np.lexsort((np.arange(infl.size), -np.abs(infl)))[:8]
+    assert np.array_equal(res["topk_pos"][0], order)
+
+
+@pytest.mark.parametrize("model", ["MF", "NCF"])
+def test_ml1m_rq1_golden(model, tmp_path):
+    f = load("ml1m_rq1_%s_k16.npz" % model.lower())
+    d = synth.make_dataset(synth.ML1M, seed=0)
+    p = synth.mf_params(d["U"], d["I"], 16, 0) if model == "MF" else synth.ncf_params(d["U"], d["I"], 16, 0)
+    m = make_model(model, d["U"], d["I"], 16, d["train"], (f["q_user"], f["q_item"]), p, tmpdir=tmp_path)
+    res = m.get_influence_batch(list(range(f["q_user"].size)), K=5)
+    assert np.array_equal(res["offsets"], f["offsets"])
+    assert np.array_equal(res["rel_idx"], f["rel"])
+    for q in range(f["q_user"].size):
+        b, e = f["offsets"][q], f["offsets"][q + 1]
+        assert rel_err(res["influence"][b:e], f["influence"][b:e]) < RTOL
+        assert rel_err(res["x"][q], f["x"][q]) < RTOL
+        assert np.array_equal(res["topk_pos"][q], f["topk_pos"][q])
+
+
+@pytest.fixture(scope="module")
+def ml1m_full(tmp_path_factory):
+    d = synth.make_dataset(synth.ML1M, seed=0)
+    p = synth.mf_params(d["U"], d["I"], 16, 0)
+    qu, qi, _ = d["test"]
+    m = make_model("MF", d["U"], d["I"], 16, d["train"], (qu, qi), p, tmpdir=tmp_path_factory.mktemp("ml"))
+    res = m.get_influence_batch(list(range(qu.size)), K=4)
+    return d, p, m, res
+
+
+def test_ml1m_all_queries_properties(ml1m_full):
+    """Config 2 (all 12,074 ml-1m-ex test ratings): offsets = deg(u)+deg(i), related
+    lists are the ascending user rows then item rows, top-K agrees with the full
+    vectors under the tie rule, and a sample of queries matches the oracle."""
+    from oracle import fia_oracle as fo
+    d, p, m, res = ml1m_full
+    tu, ti, tr = d["train"]
+    qu, qi, _ = d["test"]
+    deg_u = np.bincount(tu, minlength=d["U"])
+    deg_i = np.bincount(ti, minlength=d["I"])
+    n = deg_u[qu] + deg_i[qi]
+    assert np.array_equal(np.diff(res["offsets"]), n)
+    rel, infl = res["rel_idx"], res["influence"]
+    assert np.isfinite(infl).all()
+    offs = res["offsets"]
+    rng = np.random.default_rng(0)
+    for q in rng.choice(qu.size, 40, replace=False):
+        b, e = offs[q], offs[q + 1]
+        r = rel[b:e]
+        du = deg_u[qu[q]]
+        assert (np.diff(r[:du]) > 0).all() and (np.diff(r[du:]) > 0).all()
+        assert (tu[r[:du]] == qu[q]).all() and (ti[r[du:]] == qi[q]).all()
+        want = fo.topk(infl[b:e], 4)
+        assert np.array_equal(res["topk_pos"][q], want)
+    for q in rng.choice(qu.size, 12, replace=False):
+        o = fo.mf_query(p, 16, tu, ti, tr, int(qu[q]), int(qi[q]), 1e-3, 1e-6)
+        b, e = offs[q], offs[q + 1]
+        assert np.array_equal(o["rel"], rel[b:e])
+        assert rel_err(infl[b:e], o["influence"]) < RTOL
+        assert rel_err(res["x"][q], o["x"]) < RTOL
+
+
+def test_ml1m_deterministic(ml1m_full):
+    d, p, m, res = ml1m_full
+    again = m.get_influence_batch(list(range(d["test"][0].size)), K=4)
+    for key in ("rel_idx", "influence", "x", "topk_pos", "topk_val"):
+        assert np.array_equal(again[key], res[key], equal_nan=True), key
+
+
+def test_yelp_ncf_sample_matches_oracle(tmp_path):
+    """Config 3 shape (yelp-ex, NCF k=16): a query sample against the oracle."""
+    from oracle import fia_oracle as fo
+    d = synth.make_dataset(synth.YELP, seed=0)
+    p = synth.ncf_params(d["U"], d["I"], 16, 0)
+    qu, qi, _ = d["test"]
+    sel = np.random.default_rng(1).choice(qu.size, 16, replace=False)
+    m = make_model("NCF", d["U"], d["I"], 16, d["train"], (qu[sel], qi[sel]), p, tmpdir=tmp_path)
+    res = m.get_influence_batch(list(range(sel.size)), K=2)
+    tu, ti, tr = d["train"]
+    for q in range(sel.size):
+        o = fo.ncf_query(p, 16, tu, ti, tr, int(qu[sel[q]]), int(qi[sel[q]]), 1e-3, 1e-6)
+        b, e = res["offsets"][q], res["offsets"][q + 1]
+        assert np.array_equal(o["rel"], res["rel_idx"][b:e])
+        assert rel_err(res["influence"][b:e], o["influence"]) < RTOL
+        assert np.array_equal(res["topk_pos"][q], fo.topk(o["influence"], 2))
+
+
+def test_invalid_queries_raise(tmp_path):
+    from influence._lib import FIAError
+    f = load("small_mf_k16.npz")
+    qu = np.array([0, 1000], np.int32)
+    qi = np.array([0, 0], np.int32)
+    m = make_model("MF", f["U"], f["I"], f["k"], (f["train_user"], f["train_item"], f["train_rating"]),
+                   (qu, qi), params_of(f), tmpdir=tmp_path)
+    with pytest.raises(FIAError):
+        m.get_influence_batch([1], K=1)
+    with pytest.raises(FIAError):
+        m.get_influence_batch([0], K=65)
