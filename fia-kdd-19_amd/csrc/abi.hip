@@ -98,9 +98,11 @@ int fia_destroy(fia_ctx* c) {
       c->idx.side[s].rating.release();
       c->gram[s].release();
       c->l1[s].release();
+      c->idx.order[s].release();
     }
-    fia::DevBuf* bufs[] = {&c->rec, &c->coff, &c->cquery, &c->cstart, &c->cand_pos,
-                           &c->cand_val, &c->scan_tmp, &c->flag, &c->nch};
+    fia::DevBuf* bufs[] = {&c->rec,      &c->coff,     &c->cquery, &c->cstart,   &c->cand_pos,  &c->cand_val,
+                           &c->scan_tmp, &c->flag,     &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt,
+                           &c->idx.psum};
     for (auto* b : bufs) b->release();
     for (auto& v : c->events.ev)
       for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }

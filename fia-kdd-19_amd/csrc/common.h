@@ -17,6 +17,7 @@ constexpr int kScoreRows = 4;            // related ratings per scoring thread
 constexpr int kChunk = kScoreThreads * kScoreRows;   // related ratings per scoring chunk
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
+constexpr int kGramChunk = 512;          // list rows per Gram work item
 
 // Device buffer with grow-on-demand capacity (never shrinks).
 struct DevBuf {
@@ -59,7 +60,47 @@ struct Side {
 struct Index {
   int64_t N = 0, U = 0, I = 0;
   Side side[2];   // 0 = users (R_u), 1 = items (C_i)
+  DevBuf order[2];  // int32 [n_entity]: entities by list length, longest first (Gram scheduling)
+  // Gram work lists: items of <= kGramChunk list rows {entity, start, len, slot}; slot < 0 =
+  // write the entity's Gram directly, else a partial slot summed (in slot order) by a combine
+  // pass {entity, first_slot, n_slots, 0}
+  DevBuf gitems[2], gcomb[2];
+  int64_t n_gitems[2] = {0, 0}, n_gcomb[2] = {0, 0}, n_gslots[2] = {0, 0};
+  // open-addressing set of train pairs: key u*I+i -> (#rows, sum of ratings); answers
+  // "is the test pair itself a train row?" in O(1) for the Hessian's d2r term
+  DevBuf pkey;    // uint64 [pcap], ~0 = empty
+  DevBuf pcnt;    // int32  [pcap]
+  DevBuf psum;    // double [pcap]
+  int64_t pcap = 0;
   bool valid = false;
+};
+
+// ---- device helpers shared by the kernels ----
+constexpr unsigned long long kEmptyKey = ~0ull;
+
+__host__ __device__ inline unsigned long long pair_hash(unsigned long long k) {
+  k += 0x9e3779b97f4a7c15ull;
+  k = (k ^ (k >> 30)) * 0xbf58476d1ce4e5b9ull;
+  k = (k ^ (k >> 27)) * 0x94d049bb133111ebull;
+  return k ^ (k >> 31);
+}
+
+struct PairTable {
+  const unsigned long long* key;
+  const int32_t* cnt;
+  const double* sum;
+  unsigned long long mask;
+  __device__ inline void lookup(unsigned long long k, double& c, double& s) const {
+    unsigned long long h = pair_hash(k) & mask;
+    c = 0.0;
+    s = 0.0;
+    for (unsigned long long probe = 0; probe <= mask; ++probe) {
+      unsigned long long kk = key[h];
+      if (kk == k) { c = (double)cnt[h]; s = sum[h]; return; }
+      if (kk == kEmptyKey) return;
+      h = (h + 1) & mask;
+    }
+  }
 };
 
 // Parameter table pointers (device, float32, owned by the caller).
@@ -87,6 +128,7 @@ struct fia_ctx {
   fia::DevBuf gram[2];
   // NCF: per-entity layer-1 halves Pm*W1[:k] and Qm*W1[k:] (fp64) [U*k], [I*k]
   fia::DevBuf l1[2];
+  fia::DevBuf gpart[2];   // partial Grams of long lists (fp64, [n_gslots * GSP])
   bool prepared = false;
   // per-batch scratch
   fia::DevBuf rec;        // per-query scoring record (fp64)
@@ -98,6 +140,7 @@ struct fia_ctx {
   fia::DevBuf scan_tmp;   // rocprim temporary storage
   fia::DevBuf flag;       // int32 [4] device status words
   fia::DevBuf nch;        // int64 [Q+1] chunk counts
+  fia::DevBuf coupled;    // int32 [Q + 1]: count, then queries whose test pair is a train row
   bool profiling = false;
   fia::PhaseEvents events;
 };

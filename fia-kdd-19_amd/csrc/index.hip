@@ -7,6 +7,7 @@
 // with a one-time stable radix sort: inside every list train rows stay in
 // ascending order, so rel(u,i) = R_u ++ C_i is the reference's concatenation
 // bit for bit (mf:322).
+#include <algorithm>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -38,6 +39,27 @@ __global__ void k_gather_side(const int32_t* __restrict__ rows, const int32_t* _
     int32_t r = rows[j];
     other[j] = other_src[r];
     rating[j] = rating_src[r];
+  }
+}
+
+// pair set insert: one slot per distinct (u, i), counting duplicate train rows
+__global__ void k_pair_insert(const int32_t* __restrict__ user, const int32_t* __restrict__ item,
+                              const float* __restrict__ rating, int64_t N, int64_t I, unsigned long long* key,
+                              int32_t* cnt, double* sum, unsigned long long mask) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; j < N; j += stride) {
+    const unsigned long long k = (unsigned long long)user[j] * (unsigned long long)I + (unsigned long long)item[j];
+    unsigned long long h = pair_hash(k) & mask;
+    for (unsigned long long probe = 0; probe <= mask; ++probe) {
+      unsigned long long prev = atomicCAS(&key[h], kEmptyKey, k);
+      if (prev == kEmptyKey || prev == k) {
+        atomicAdd(&cnt[h], 1);
+        atomicAdd(&sum[h], (double)rating[j]);
+        break;
+      }
+      h = (h + 1) & mask;
+    }
   }
 }
 
@@ -172,9 +194,58 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
                        keys_sorted.as<int32_t>(), N, n_ent[sd], S.ptr.as<int64_t>());
     FIA_HIP_TRY(hipGetLastError());
     FIA_HIP_TRY(hipStreamSynchronize(s));   // keys_sorted is reused by the next side
+    // entities by list length, longest first: the Gram kernels start the long lists early
+    std::vector<int64_t> hptr((size_t)n_ent[sd] + 1);
+    FIA_HIP_TRY(hipMemcpy(hptr.data(), S.ptr.ptr, sizeof(int64_t) * hptr.size(), hipMemcpyDeviceToHost));
+    std::vector<int32_t> ord((size_t)n_ent[sd]);
+    for (int64_t e = 0; e < n_ent[sd]; ++e) ord[(size_t)e] = (int32_t)e;
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+      return hptr[(size_t)a + 1] - hptr[(size_t)a] > hptr[(size_t)b + 1] - hptr[(size_t)b];
+    });
+    FIA_HIP_TRY(X.order[sd].reserve(sizeof(int32_t) * ord.size()));
+    FIA_HIP_TRY(hipMemcpy(X.order[sd].ptr, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice));
+    // Gram work items (longest lists first) and the combine list of split entities
+    std::vector<int32_t> items, comb;
+    int32_t slots = 0;
+    for (int32_t e : ord) {
+      const int64_t len = hptr[(size_t)e + 1] - hptr[(size_t)e];
+      const int64_t nit = len == 0 ? 1 : (len + kGramChunk - 1) / kGramChunk;
+      if (nit > 1) comb.insert(comb.end(), {e, slots, (int32_t)nit, 0});
+      for (int64_t t = 0; t < nit; ++t) {
+        const int64_t st = t * kGramChunk;
+        const int64_t ln = std::min<int64_t>(kGramChunk, len - st);
+        items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), nit > 1 ? slots++ : -1});
+      }
+    }
+    X.n_gitems[sd] = (int64_t)items.size() / 4;
+    X.n_gcomb[sd] = (int64_t)comb.size() / 4;
+    X.n_gslots[sd] = slots;
+    FIA_HIP_TRY(X.gitems[sd].reserve(sizeof(int32_t) * items.size()));
+    FIA_HIP_TRY(hipMemcpy(X.gitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+    if (!comb.empty()) {
+      FIA_HIP_TRY(X.gcomb[sd].reserve(sizeof(int32_t) * comb.size()));
+      FIA_HIP_TRY(hipMemcpy(X.gcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
+    }
   }
   keys_sorted.release();
   tmp.release();
+  // pair set, load factor <= 1/2
+  int64_t cap = 1024;
+  while (cap < 2 * N) cap <<= 1;
+  FIA_HIP_TRY(X.pkey.reserve(sizeof(unsigned long long) * (size_t)cap));
+  FIA_HIP_TRY(X.pcnt.reserve(sizeof(int32_t) * (size_t)cap));
+  FIA_HIP_TRY(X.psum.reserve(sizeof(double) * (size_t)cap));
+  FIA_HIP_TRY(hipMemsetAsync(X.pkey.ptr, 0xff, sizeof(unsigned long long) * (size_t)cap, s));
+  FIA_HIP_TRY(hipMemsetAsync(X.pcnt.ptr, 0, sizeof(int32_t) * (size_t)cap, s));
+  FIA_HIP_TRY(hipMemsetAsync(X.psum.ptr, 0, sizeof(double) * (size_t)cap, s));
+  if (N > 0) {
+    hipLaunchKernelGGL(k_pair_insert, dim3(grid_for(N, 256)), dim3(256), 0, s, user, item, rating, N, I,
+                       X.pkey.as<unsigned long long>(), X.pcnt.as<int32_t>(), X.psum.as<double>(),
+                       (unsigned long long)(cap - 1));
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  FIA_HIP_TRY(hipStreamSynchronize(s));
+  X.pcap = cap;
   X.N = N;
   X.U = U;
   X.I = I;

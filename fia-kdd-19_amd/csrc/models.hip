@@ -30,8 +30,8 @@ struct MFm {
   static constexpr int K = K_;
   static constexpr int Ds = K + 1;
   static constexpr int D = 2 * Ds;
-  static constexpr int SB = 2 * K + 4;          // per-side record: a, xs, bias, xsb, dup_extra, dup_other
-  static constexpr int R = 2 + 2 * SB;
+  static constexpr int SB = 2 * K + 3;          // per-side record: a, xs, bias, xsb, dup_other
+  static constexpr int R = 4 + 2 * SB;          // header: inv_n, c_q, x.v, r-hat(u,i)
   static constexpr bool ncf = false;
   __device__ static bool decayed(int a) { return a < K; }
   // reference theta order [p_u, q_i, b_u, b_i]
@@ -47,8 +47,8 @@ struct NCFm {
   static constexpr int H2 = K / 2;
   static constexpr int Ds = 2 * K;
   static constexpr int D = 2 * Ds;
-  static constexpr int SB = 4 * K + 2;          // per-side record: tself, yv, bx, ag, dup_extra, dup_other
-  static constexpr int R = 2 + 2 * SB;
+  static constexpr int SB = 4 * K + 1;          // per-side record: tself, yv, bx, ag, dup_other
+  static constexpr int R = 4 + 2 * SB;          // header: inv_n, c_q, x.v, r-hat(u,i)
   static constexpr bool ncf = true;
   __device__ static bool decayed(int) { return true; }
   // reference theta order [Pm_u, Qm_i, Pg_u, Qg_i]
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_gram(
       }
     }
   }
-  double* out = gram + e * GS;
+  double* out = gram + e * ((GS + 1) & ~1);
 #pragma unroll
   for (int m = 0; m < MAXE; ++m) {
     int idx = tid + m * kPrepThreads;
@@ -357,17 +357,22 @@ struct QueryArgs {
   const double* l1[2];
   const float* t[10];
   double wd, damping;
+  PairTable pairs;
 };
 
+// One wave per query (general D; the path for NCF, MF k >= 32 and for queries whose
+// test pair is itself a train row).  qlist (nullable): {count, q_0, q_1, ...}.
 template <class M>
 __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                                         double* __restrict__ x_out) {
+                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
   __shared__ double H[D * (D + 1) / 2];
   __shared__ double v[D], g[D], th[D], dd[D], ww[D];
   __shared__ double sh[4 * K + 8];
-  const int64_t q = blockIdx.x;
-  if (q >= Q) return;
+  const int64_t nwork = qlist ? (int64_t)qlist[0] : Q;
+  for (int64_t wk = blockIdx.x; wk < nwork; wk += gridDim.x) {
+  __syncthreads();
+  const int64_t q = qlist ? (int64_t)qlist[1 + wk] : wk;
   const int lane = threadIdx.x;
   const int32_t u = A.qu[q], i = A.qi[q];
   double* R = rec + q * M::R;
@@ -379,7 +384,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
     if (x_out)
       for (int a = lane; a < D; a += kSolveThreads) x_out[q * D + a] = NAN;
     if (lane == 0) R[0] = NAN;
-    return;
+    continue;
   }
   const double s2n = 2.0 / (double)n;
 
@@ -457,25 +462,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
   }
   __syncthreads();
 
-  // ---- the (u,i) pair among the train rows: scan the shorter list ----
-  double cdup = 0.0, rsum = 0.0;
-  {
-    const int sd = du <= di ? 0 : 1;
-    const int64_t lb = sd == 0 ? ub : ib, ln = sd == 0 ? du : di;
-    const int32_t want = sd == 0 ? i : u;
-    const int32_t* oth = A.other[sd] + lb;
-    const float* rt = A.rating[sd] + lb;
-    for (int64_t p = lane; p < ln; p += kSolveThreads)
-      if (oth[p] == want) { cdup += 1.0; rsum += (double)rt[p]; }
-    cdup = wave_sum(cdup);
-    rsum = wave_sum(rsum);
-  }
+  // ---- the (u,i) pair among the train rows (pair set built with the index) ----
+  double cdup, rsum;
+  A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
   const bool coupled = cdup > 0.0;
   const double esum = cdup * rhat_ui - rsum;
 
   // ---- assemble H (packed lower, D x D) ----
-  const double* Gu = A.gram[0] + (int64_t)u * GS;
-  const double* Gi = A.gram[1] + (int64_t)i * GS;
+  const double* Gu = A.gram[0] + (int64_t)u * ((GS + 1) & ~1);
+  const double* Gi = A.gram[1] + (int64_t)i * ((GS + 1) & ~1);
   for (int t = lane; t < D * (D + 1) / 2; t += kSolveThreads) {
     int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
     while (tri(r + 1, 0) <= t) ++r;
@@ -523,12 +518,17 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
   cq = wave_sum(cq) * A.wd;
   xg_user = wave_sum(xg_user);
   xg_item = wave_sum(xg_item);
+  // The (u,i) train row itself has g = v, so x.g = x.v and e = r-hat(u,i) - y: both of
+  // its copies in rel (user side and item side) get bit-identical influence, as the
+  // reference's per-row sess.run gives them (mf:240-246).
   if (lane == 0) {
     R[0] = 1.0 / (double)n;
     R[1] = cq;
+    R[2] = xg_user + xg_item;
+    R[3] = rhat_ui;
   }
-  double* S0 = R + 2;
-  double* S1 = R + 2 + M::SB;
+  double* S0 = R + 4;
+  double* S1 = R + 4 + M::SB;
   if constexpr (!M::ncf) {
     const double gb = (double)A.t[4][0];
     for (int a = lane; a < K; a += kSolveThreads) {
@@ -540,8 +540,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
     if (lane == 0) {
       S0[2 * K] = th[K] + gb;     S1[2 * K] = th[Ds + K] + gb;
       S0[2 * K + 1] = v[K];       S1[2 * K + 1] = v[Ds + K];
-      S0[2 * K + 2] = xg_item;    S1[2 * K + 2] = xg_user;
-      S0[2 * K + 3] = (double)i;  S1[2 * K + 3] = (double)u;
+      S0[2 * K + 2] = (double)i;  S1[2 * K + 2] = (double)u;
     }
   } else {
     constexpr int H2 = K / 2;
@@ -565,9 +564,228 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
       S1[3 * K + c] = w3g * th[Ds + K + c];
     }
     if (lane == 0) {
-      S0[4 * K] = xg_item;   S1[4 * K] = xg_user;
-      S0[4 * K + 1] = (double)i;  S1[4 * K + 1] = (double)u;
+      S0[4 * K] = (double)i;  S1[4 * K] = (double)u;
     }
+  }
+  }   // work loop
+}
+
+// ------------------------------------------------------------------------------------
+// MF, k <= 16: thread-per-system solve.  Every lane owns one (query, side) block of
+// H_t (user block for even lanes, item block for odd lanes) and factors it with
+// LDL^T entirely in registers (153 doubles at k=16, fully unrolled), then solves.  A
+// query whose test pair is a train row couples the blocks: it is appended to the
+// `coupled` list and solved afterwards by k_solve (one wave, full D).
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double* __restrict__ rec,
+                                                  double* __restrict__ x_out, int32_t* __restrict__ coupled) {
+  static_assert(!M::ncf, "thread-per-system solve is the MF path");
+  constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  const int lane = threadIdx.x;
+  const int64_t sys = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t q = sys >> 1;
+  const int side = (int)(sys & 1);
+  const bool active = q < Q;
+  int32_t u = 0, i = 0;
+  int64_t n = 0;
+  if (active) {
+    u = A.qu[q];
+    i = A.qi[q];
+    if (u >= 0 && u < A.U && i >= 0 && i < A.I)
+      n = (A.ptr[0][u + 1] - A.ptr[0][u]) + (A.ptr[1][i + 1] - A.ptr[1][i]);
+    else
+      u = i = 0;
+  }
+  double cdup = 0.0, rsum = 0.0;
+  if (active && n > 0)
+    A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
+  if (active && n > 0 && cdup > 0.0 && side == 0) {
+    const int slot = atomicAdd(coupled, 1);
+    coupled[1 + slot] = (int32_t)q;
+  }
+  if (active && n == 0) {
+    if (x_out)
+      for (int a = 0; a < Ds; ++a) x_out[q * D + M::ref_index(side * Ds + a)] = NAN;
+    if (side == 0) rec[q * M::R] = NAN;
+  }
+  const bool work = active && n > 0 && cdup == 0.0;
+  const int32_t ent = side == 0 ? u : i;       // this block's entity
+  const int32_t oth = side == 0 ? i : u;       // the other endpoint of the test pair
+  const float* Eself = side == 0 ? A.t[0] : A.t[1];
+  const float* Eoth = side == 0 ? A.t[1] : A.t[0];
+  const float* Bself = side == 0 ? A.t[2] : A.t[3];
+
+  // H block = (2/n) Gram + wd on the embedding coordinates + damping
+  const double s2n = n > 0 ? 2.0 / (double)n : 0.0;
+  const double* G = A.gram[side] + (int64_t)ent * GSP;
+  // the whole packed block lives in registers: fully unrolled, every index constant
+  double h[GS];
+#define HS(t) h[(t)]
+#pragma unroll
+  for (int t = 0; t < GS; ++t) HS(t) = s2n * G[t];
+#pragma unroll
+  for (int r = 0; r < Ds; ++r) HS(tri(r, r)) += (r < K ? A.wd : 0.0) + A.damping;
+
+  // right-looking LDL^T: column j holds L[., j], the diagonal holds d
+#pragma unroll
+  for (int j = 0; j < Ds; ++j) {
+    const double inv = 1.0 / HS(tri(j, j));
+#pragma unroll
+    for (int r = j + 1; r < Ds; ++r) {
+      const double lr = HS(tri(r, j)) * inv;
+#pragma unroll
+      for (int c = j + 1; c <= r; ++c) HS(tri(r, c)) = fma(-lr, HS(tri(c, j)), HS(tri(r, c)));
+    }
+#pragma unroll
+    for (int r = j + 1; r < Ds; ++r) HS(tri(r, j)) *= inv;
+  }
+  // v block: user side [q_i ; 1], item side [p_u ; 1]  (gnn:155, mf:194)
+  double x[Ds];
+  load_row_f32<K>(Eoth + (int64_t)oth * K, x);
+  x[K] = 1.0;
+#pragma unroll
+  for (int j = 0; j < Ds; ++j)
+#pragma unroll
+    for (int r = j + 1; r < Ds; ++r) x[r] = fma(-HS(tri(r, j)), x[j], x[r]);
+#pragma unroll
+  for (int j = 0; j < Ds; ++j) x[j] /= HS(tri(j, j));
+#pragma unroll
+  for (int j = Ds - 1; j >= 0; --j)
+#pragma unroll
+    for (int c = 0; c < j; ++c) x[c] = fma(-HS(tri(j, c)), x[j], x[c]);
+#undef HS
+
+  // record pieces: theta block, x.v, wd x.theta, r-hat(u,i)
+  double th[K], vv[K];
+  load_row_f32<K>(Eself + (int64_t)ent * K, th);
+  load_row_f32<K>(Eoth + (int64_t)oth * K, vv);
+  const double bself = (double)Bself[ent];
+  const double gb = (double)A.t[4][0];
+  double cq = 0.0, xg = x[K], pv = 0.0;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    cq = fma(x[a], th[a], cq);
+    xg = fma(x[a], vv[a], xg);
+    pv = fma(th[a], vv[a], pv);
+  }
+  cq *= A.wd;
+  cq += __shfl_xor(cq, 1);
+  xg += __shfl_xor(xg, 1);
+  const double bpair = bself + __shfl_xor(bself, 1);
+  if (!work) return;
+  double* R = rec + q * M::R;
+  if (side == 0) {
+    R[0] = 1.0 / (double)n;
+    R[1] = cq;
+    R[2] = xg;
+    R[3] = pv + bpair + gb;        // r-hat(u,i)
+  }
+  double* S = R + 4 + side * M::SB;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    S[a] = th[a];
+    S[K + a] = x[a];
+  }
+  S[2 * K] = bself + gb;
+  S[2 * K + 1] = x[K];
+  S[2 * K + 2] = (double)oth;
+  if (x_out)
+#pragma unroll
+    for (int a = 0; a < Ds; ++a) x_out[q * D + M::ref_index(side * Ds + a)] = x[a];
+}
+
+// ------------------------------------------------------------------------------------
+// MF Gram on the f64 matrix cores: one wave per entity, 4 list rows per
+// v_mfma_f64_16x16x4_f64.  Lane l holds G[t0 + l/16][16 c + l%16] of the gathered
+// other-side embeddings, which is both the A (= G^T) and the B operand of
+// C += G^T G; the bias row (sums) and count come from VALU adds.
+// C/D map (f64 16x16x4): col = l & 15, row = (l >> 4) + 4 r.
+// ------------------------------------------------------------------------------------
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
+template <class M>
+__global__ __launch_bounds__(64) void k_gram_mf_mfma(int64_t n_items, const int32_t* __restrict__ items,
+                                                     const int64_t* __restrict__ ptr,
+                                                     const int32_t* __restrict__ other,
+                                                     const float* __restrict__ emb_other, double* __restrict__ gram,
+                                                     double* __restrict__ part) {
+  constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  constexpr int NT = (K + 15) / 16;               // 16-wide column tiles
+  constexpr int NP = NT * (NT + 1) / 2;           // upper tile pairs
+  constexpr int SUB = NT <= 2 ? 16 : 8;           // MFMA row-quads gathered ahead per batch
+  const int64_t w = blockIdx.x;
+  if (w >= n_items) return;
+  const int32_t e = items[4 * w], start = items[4 * w + 1], len = items[4 * w + 2], slot = items[4 * w + 3];
+  const int lane = threadIdx.x;
+  const int col = lane & 15, grp = lane >> 4;
+  const int32_t* ids = other + ptr[e] + start;
+  d4_t acc[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
+  double sum[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) sum[t] = 0.0;
+  for (int t0 = 0; t0 < len; t0 += 4 * SUB) {
+    // one coalesced load of 4*SUB row ids, then every row-quad's gather in flight at once
+    const int my = t0 + lane;
+    const int32_t id = (lane < 4 * SUB && my < len) ? ids[my] : -1;
+    double val[SUB][NT];
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      const int32_t o = __shfl(id, 4 * sb + grp);
+      const float* src = emb_other + (int64_t)(o < 0 ? 0 : o) * K;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) val[sb][t] = (o >= 0 && 16 * t + col < K) ? (double)src[16 * t + col] : 0.0;
+    }
+#pragma unroll
+    for (int sb = 0; sb < SUB; ++sb) {
+      int p = 0;
+#pragma unroll
+      for (int ta = 0; ta < NT; ++ta) {
+        sum[ta] += val[sb][ta];
+#pragma unroll
+        for (int tb = ta; tb < NT; ++tb, ++p)
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(val[sb][ta], val[sb][tb], acc[p], 0, 0, 0);
+      }
+    }
+  }
+  double* out = slot < 0 ? gram + (int64_t)e * GSP : part + (int64_t)slot * GSP;
+  int p = 0;
+#pragma unroll
+  for (int ta = 0; ta < NT; ++ta) {
+#pragma unroll
+    for (int tb = ta; tb < NT; ++tb, ++p) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int ci = 16 * ta + grp + 4 * rr;    // C row -> Gram column index (tile ta)
+        const int rj = 16 * tb + col;             // C col -> Gram row index (tile tb)
+        if (ci < K && rj < K && rj >= ci) out[tri(rj, ci)] = acc[p][rr];
+      }
+    }
+  }
+  // bias row: Gram[K][c] = sum over rows of G[.][c]; Gram[K][K] = row count
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    double s = sum[t];
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (grp == 0 && 16 * t + col < K) out[tri(K, 16 * t + col)] = s;
+  }
+  if (lane == 0) out[tri(K, K)] = (double)len;
+}
+
+// Sum the partial Grams of split lists in slot order (deterministic).
+__global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb, const int32_t* __restrict__ comb, int GS,
+                                                     int GSP, const double* __restrict__ part,
+                                                     double* __restrict__ gram) {
+  const int64_t w = blockIdx.x;
+  if (w >= n_comb) return;
+  const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
+  for (int t = threadIdx.x; t < GS; t += 64) {
+    double s = 0.0;
+    for (int k = 0; k < ns; ++k) s += part[(int64_t)(first + k) * GSP + t];
+    gram[(int64_t)e * GSP + t] = s;
   }
 }
 
@@ -599,10 +817,25 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
     const int64_t ib = A.ptr[1][i];
     const int64_t base = offsets[q];
     const int64_t n = offsets[q + 1] - base;
+    // list entries first: they do not depend on the query record
+    int32_t o_[kScoreRows], row_[kScoreRows];
+    float y_[kScoreRows];
+#pragma unroll
+    for (int rr = 0; rr < kScoreRows; ++rr) {
+      const int64_t p = (int64_t)start + rr * kScoreThreads + tid;
+      o_[rr] = -1;
+      if (p < n) {
+        const int sd = p < du ? 0 : 1;
+        const int64_t li = sd == 0 ? ub + p : ib + (p - du);
+        o_[rr] = A.other[sd][li];
+        y_[rr] = A.rating[sd][li];
+        row_[rr] = A.row[sd][li];
+      }
+    }
     __syncthreads();
     for (int t = tid; t < M::R; t += kScoreThreads) sr[t] = rec[(int64_t)q * M::R + t];
     __syncthreads();
-    const double inv_n = sr[0], cq = sr[1];
+    const double inv_n = sr[0], cq = sr[1], xv = sr[2], rhat_ui = sr[3];
     double ca[kScoreRows], cv[kScoreRows];
     int cp[kScoreRows];
 #pragma unroll
@@ -613,11 +846,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
       cv[rr] = 0.0;
       if (p >= n) continue;
       const int sd = p < du ? 0 : 1;
-      const int64_t li = sd == 0 ? ub + p : ib + (p - du);
-      const int32_t o = A.other[sd][li];
-      const double y = (double)A.rating[sd][li];
-      const double* S = sr + 2 + sd * M::SB;
-      double infl;
+      const int32_t o = o_[rr];
+      const double y = (double)y_[rr];
+      const double* S = sr + 4 + sd * M::SB;
+      double e, s;
       if constexpr (!M::ncf) {
         // other-side embedding and bias: side 0 (user rows) -> item tables, side 1 -> user tables
         const float* T = sd == 0 ? A.t[1] : A.t[0];
@@ -630,12 +862,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
           dot_a = fma(S[c], row_e[c], dot_a);
           dot_x = fma(S[K + c], row_e[c], dot_x);
         }
-        const double e = dot_a + S[2 * K] + (double)bt[o] - y;
-        double s = dot_x + S[2 * K + 1];
-        if ((double)o == S[2 * K + 3]) s += S[2 * K + 2];
-        infl = (2.0 * e * s + cq) * inv_n;
+        e = dot_a + S[2 * K] + (double)bt[o] - y;
+        s = dot_x + S[2 * K + 1];
+        if ((double)o == S[2 * K + 2]) { e = rhat_ui - y; s = xv; }
       } else {
-        constexpr int H2 = K / 2;
         const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o * K;
         const float* G = (sd == 0 ? A.t[3] : A.t[2]) + (int64_t)o * K;   // other side gmf row
         double z1[K], d1[K], grow[K];
@@ -643,20 +873,20 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
         for (int c = 0; c < K; ++c) z1[c] = S[c] + L1o[c];
         const double mlp = ncf_mlp<K>(w, z1, d1);
         load_row_f32<K>(G, grow);
-        double gmf = 0.0, s = 0.0;
+        double gmf = 0.0;
+        s = 0.0;
 #pragma unroll
         for (int c = 0; c < K; ++c) {
           s = fma(S[K + c], d1[c], s);
           s = fma(S[2 * K + c], grow[c], s);
           gmf = fma(S[3 * K + c], grow[c], gmf);
         }
-        (void)H2;
-        const double e = mlp + gmf + (double)A.t[9][0] - y;
-        if ((double)o == S[4 * K + 1]) s += S[4 * K];
-        infl = (2.0 * e * s + cq) * inv_n;
+        e = mlp + gmf + (double)A.t[9][0] - y;
+        if ((double)o == S[4 * K]) { e = rhat_ui - y; s = xv; }
       }
+      const double infl = (2.0 * e * s + cq) * inv_n;
       if (influence) influence[base + p] = infl;
-      if (rel_idx) rel_idx[base + p] = A.row[sd][li];
+      if (rel_idx) rel_idx[base + p] = row_[rr];
       cp[rr] = (int)p;
       ca[rr] = topk_key(infl);
       cv[rr] = infl;
@@ -727,14 +957,23 @@ QueryArgs make_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
   for (int t = 0; t < 10; ++t) A.t[t] = c->p.t[t];
   A.wd = c->p.wd;
   A.damping = c->p.damping;
+  A.pairs.key = c->idx.pkey.as<unsigned long long>();
+  A.pairs.cnt = c->idx.pcnt.as<int32_t>();
+  A.pairs.sum = c->idx.psum.as<double>();
+  A.pairs.mask = (unsigned long long)(c->idx.pcap - 1);
   return A;
+}
+
+template <class M>
+constexpr bool use_tps() {
+  return !M::ncf && M::Ds <= 17;
 }
 
 template <class M>
 hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   constexpr int Ds = M::Ds, GS = Ds * (Ds + 1) / 2, K = M::K;
   const int64_t n_ent[2] = {c->p.U, c->p.I};
-  for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * GS + 1)));
+  for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * ((GS + 1) & ~1) + 1)));
   if constexpr (M::ncf) {
     for (int sd = 0; sd < 2; ++sd) {
       FIA_HIP_TRY(c->l1[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * K + 1)));
@@ -751,6 +990,21 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
     const float* emb_other;
     if constexpr (M::ncf) emb_other = c->p.t[sd == 0 ? 3 : 2];   // gmf table of the other side
     else emb_other = c->p.t[sd == 0 ? 1 : 0];
+    if constexpr (!M::ncf) {
+      constexpr int GSP = (GS + 1) & ~1;
+      const Index& X = c->idx;
+      if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
+      hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)X.n_gitems[sd]), dim3(64), 0, s, X.n_gitems[sd],
+                         X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
+                         emb_other, c->gram[sd].as<double>(), c->gpart[sd].as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+      if (X.n_gcomb[sd] > 0) {
+        hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)X.n_gcomb[sd]), dim3(64), 0, s, X.n_gcomb[sd],
+                           X.gcomb[sd].as<int32_t>(), GS, GSP, c->gpart[sd].as<double>(), c->gram[sd].as<double>());
+        FIA_HIP_TRY(hipGetLastError());
+      }
+      continue;
+    }
     hipLaunchKernelGGL(k_gram<M>, dim3((unsigned)n_ent[sd]), dim3(kPrepThreads), 0, s, sd, n_ent[sd],
                        c->idx.side[sd].ptr.as<int64_t>(), c->idx.side[sd].other.as<int32_t>(), emb_other,
                        c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4], c->p.t[5], c->p.t[6],
@@ -774,7 +1028,19 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   FIA_HIP_TRY(build_chunks(c, Q, offsets, max_chunks, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
-  hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)Q), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out);
+  if constexpr (use_tps<M>()) {
+    FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
+    FIA_HIP_TRY(hipMemsetAsync(c->coupled.ptr, 0, sizeof(int32_t), s));
+    hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
+                       c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+    FIA_HIP_TRY(hipGetLastError());
+    const int64_t g2 = Q < 1024 ? Q : 1024;
+    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
+                       (const int32_t*)c->coupled.as<int32_t>());
+  } else {
+    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)Q), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
+                       (const int32_t*)nullptr);
+  }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
   int64_t grid = max_chunks < 1 ? 1 : max_chunks;

@@ -48,6 +48,29 @@ def rel_err(a, b):
     return np.abs(a - b).max(initial=0.0) / (s if s > 0 else 1.0)
 
 
+NEAR_TIE = 1e-12
+
+
+def check_topk(got, gpu_vals, oracle_vals, K):
+    """Top-K positions: (1) bit-exact selection on the kernel's own fp64 values;
+    (2) bit-exact against the oracle's ranking, except that two entries whose
+    |oracle value| differ by < 1e-12 * max may swap (near-ties are flagged, not
+    failed: SURVEY.md 8c).  Returns the number of near-tie swaps."""
+    from oracle import fia_oracle as fo
+    want_gpu = fo.topk(gpu_vals, K)
+    assert np.array_equal(got[:want_gpu.size], want_gpu)
+    assert (got[want_gpu.size:] == -1).all()
+    want = fo.topk(oracle_vals, K)
+    assert want.size == want_gpu.size
+    a = np.abs(oracle_vals)
+    tol = NEAR_TIE * a.max(initial=0.0)
+    swaps = 0
+    for t in np.nonzero(got[:want.size] != want)[0]:
+        assert abs(a[got[t]] - a[want[t]]) <= tol, (t, got[t], want[t], a[got[t]], a[want[t]])
+        swaps += 1
+    return swaps
+
+
 @pytest.mark.parametrize("name", ["small_mf_k16.npz", "small_ncf_k16.npz", "small_mf_k8.npz", "small_ncf_k8.npz"])
 def test_small_golden_single_query_api(name, tmp_path):
     f = load(name)
@@ -85,10 +108,10 @@ def test_small_golden_batch_and_topk(name, K, tmp_path):
         b, e = f["offsets"][q], f["offsets"][q + 1]
         if e > b:
             assert rel_err(res["influence"][b:e], f["influence"][b:e]) < RTOL
-        want = fo.topk(f["influence"][b:e], K)
         got = res["topk_pos"][q]
-        assert np.array_equal(got[:want.size], want)
-        assert (got[want.size:] == -1).all() and np.isnan(res["topk_val"][q][want.size:]).all()
+        check_topk(got, res["influence"][b:e], f["influence"][b:e], K)
+        want = got[got >= 0]
+        assert np.isnan(res["topk_val"][q][want.size:]).all()
         assert np.array_equal(res["topk_idx"][q][:want.size], f["rel"][b:e][want])
         np.testing.assert_array_equal(res["topk_val"][q][:want.size], res["influence"][b:e][want])
 
@@ -102,6 +125,11 @@ def test_duplicate_rows_tie_by_position(tmp_path):
     q = 2   # (tu[7], ti[7]) duplicated in train
     res = m.get_influence_batch([q], K=8)
     infl = res["influence"]
+    rel = res["rel_idx"]
+    for row in np.unique(rel):
+        copies = infl[rel == row]
+        assert (copies == copies[0]).all()          # each copy of a train row: identical bits
+    assert (np.bincount(rel) == 2).sum() == 2       # both (u,i) rows appear twice
     order = np.lexsort((np.arange(infl.size), -np.abs(infl)))[:8]
     assert np.array_equal(res["topk_pos"][0], order)
 
@@ -119,6 +147,7 @@ def test_ml1m_rq1_golden(model, tmp_path):
         b, e = f["offsets"][q], f["offsets"][q + 1]
         assert rel_err(res["influence"][b:e], f["influence"][b:e]) < RTOL
         assert rel_err(res["x"][q], f["x"][q]) < RTOL
+        check_topk(res["topk_pos"][q], res["influence"][b:e], f["influence"][b:e], 5)
         assert np.array_equal(res["topk_pos"][q], f["topk_pos"][q])
 
 
@@ -162,6 +191,7 @@ def test_ml1m_all_queries_properties(ml1m_full):
         assert np.array_equal(o["rel"], rel[b:e])
         assert rel_err(infl[b:e], o["influence"]) < RTOL
         assert rel_err(res["x"][q], o["x"]) < RTOL
+        check_topk(res["topk_pos"][q], infl[b:e], o["influence"], 4)
 
 
 def test_ml1m_deterministic(ml1m_full):
@@ -186,7 +216,7 @@ def test_yelp_ncf_sample_matches_oracle(tmp_path):
         b, e = res["offsets"][q], res["offsets"][q + 1]
         assert np.array_equal(o["rel"], res["rel_idx"][b:e])
         assert rel_err(res["influence"][b:e], o["influence"]) < RTOL
-        assert np.array_equal(res["topk_pos"][q], fo.topk(o["influence"], 2))
+        check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], 2)
 
 
 def test_invalid_queries_raise(tmp_path):
