@@ -100,7 +100,7 @@ int fia_destroy(fia_ctx* c) {
       c->l1[s].release();
       c->idx.order[s].release();
     }
-    fia::DevBuf* bufs[] = {&c->rec,      &c->coff,     &c->cquery, &c->cstart,   &c->cand_pos,  &c->cand_val,
+    fia::DevBuf* bufs[] = {&c->rec,      &c->coff,     &c->cdesc,                &c->cand_pos,  &c->cand_val,
                            &c->scan_tmp, &c->flag,     &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt,
                            &c->idx.psum};
     for (auto* b : bufs) b->release();
@@ -244,7 +244,7 @@ int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
     if (K > 0 && (!topk_pos || !topk_idx || !topk_val)) return fail(c, FIA_ERR_INVALID, "null top-K output");
     if (Q == 0) return FIA_OK;
     DeviceGuard g(c->device);
-    const int64_t max_chunks = Q + total_rel / fia::kChunk + 1;
+    const int64_t max_chunks = 2 * Q + total_rel / fia::kChunk + 1;
     bool unsup = false;
     hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,
                                     topk_idx, topk_val, as_stream(stream), unsup);

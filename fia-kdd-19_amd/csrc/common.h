@@ -12,9 +12,20 @@
 namespace fia {
 
 constexpr int kWave = 64;
-constexpr int kScoreThreads = 256;       // scoring workgroup
-constexpr int kScoreRows = 4;            // related ratings per scoring thread
-constexpr int kChunk = kScoreThreads * kScoreRows;   // related ratings per scoring chunk
+constexpr int kScoreThreads = 256;       // scoring workgroup (4 independent waves)
+constexpr int kScoreRows = 4;            // related ratings per lane and chunk
+constexpr int kChunk = 64 * kScoreRows;  // related ratings per scoring chunk (one wave)
+
+// One scoring chunk: <= kChunk consecutive ratings of ONE side (user list or item
+// list) of one query, so every value a wave needs from the query is wave-uniform.
+struct ChunkDesc {
+  int64_t list_base;   // index into the side's list arrays
+  int64_t out_base;    // index into rel_idx / influence
+  int32_t q;           // query
+  int32_t pos0;        // related position of the chunk's first rating
+  int32_t len;         // ratings in the chunk
+  int32_t side;        // 0 = user list R_u, 1 = item list C_i
+};
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 512;          // list rows per Gram work item
@@ -133,8 +144,7 @@ struct fia_ctx {
   // per-batch scratch
   fia::DevBuf rec;        // per-query scoring record (fp64)
   fia::DevBuf coff;       // int64 [Q+1] chunk offsets
-  fia::DevBuf cquery;     // int32 [max chunks]
-  fia::DevBuf cstart;     // int32 [max chunks]
+  fia::DevBuf cdesc;      // ChunkDesc [max chunks]
   fia::DevBuf cand_pos;   // int32 [max chunks * K]
   fia::DevBuf cand_val;   // double [max chunks * K]
   fia::DevBuf scan_tmp;   // rocprim temporary storage
@@ -154,7 +164,8 @@ hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
                          int64_t* offsets, hipStream_t s);
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
                          const int64_t* offsets, int64_t* rel, hipStream_t s);
-hipError_t build_chunks(fia_ctx* c, int64_t Q, const int64_t* offsets, int64_t max_chunks, hipStream_t s);
+hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                        int64_t max_chunks, hipStream_t s);
 hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
 
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`

@@ -89,22 +89,60 @@ __global__ void k_count(const int32_t* __restrict__ qu, const int32_t* __restric
   counts[q] = n;
 }
 
-__global__ void k_chunk_counts(const int64_t* __restrict__ offsets, int64_t Q, int64_t* __restrict__ nch) {
+__device__ inline void query_sides(const int32_t* qu, const int32_t* qi, int64_t q, const int64_t* uptr,
+                                   const int64_t* iptr, int64_t U, int64_t I, int64_t& ub, int64_t& du, int64_t& ib,
+                                   int64_t& di) {
+  const int32_t u = qu[q], i = qi[q];
+  ub = du = ib = di = 0;
+  if (u >= 0 && u < U && i >= 0 && i < I) {
+    ub = uptr[u];
+    du = uptr[u + 1] - ub;
+    ib = iptr[i];
+    di = iptr[i + 1] - ib;
+  }
+}
+
+// chunks per query: ceil(|R_u| / kChunk) + ceil(|C_i| / kChunk)
+__global__ void k_chunk_counts(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
+                               const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U,
+                               int64_t I, int64_t* __restrict__ nch) {
   int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q > Q) return;
   if (q == Q) { nch[Q] = 0; return; }
-  int64_t n = offsets[q + 1] - offsets[q];
-  nch[q] = (n + kChunk - 1) / kChunk;
+  int64_t ub, du, ib, di;
+  query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
+  nch[q] = (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
 }
 
-__global__ void k_chunk_fill(const int64_t* __restrict__ coff, int64_t Q, int32_t* __restrict__ cquery,
-                             int32_t* __restrict__ cstart) {
+__global__ void k_chunk_fill(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
+                             const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
+                             const int64_t* __restrict__ offsets, const int64_t* __restrict__ coff,
+                             ChunkDesc* __restrict__ cdesc) {
   int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Q) return;
-  int64_t b = coff[q], e = coff[q + 1];
-  for (int64_t c = b; c < e; ++c) {
-    cquery[c] = (int32_t)q;
-    cstart[c] = (int32_t)((c - b) * kChunk);
+  int64_t ub, du, ib, di;
+  query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
+  int64_t c = coff[q];
+  const int64_t base = offsets[q];
+  for (int64_t st = 0; st < du; st += kChunk, ++c) {
+    ChunkDesc d;
+    d.list_base = ub + st;
+    d.out_base = base + st;
+    d.q = (int32_t)q;
+    d.pos0 = (int32_t)st;
+    d.len = (int32_t)(du - st < kChunk ? du - st : kChunk);
+    d.side = 0;
+    cdesc[c] = d;
+  }
+  for (int64_t st = 0; st < di; st += kChunk, ++c) {
+    ChunkDesc d;
+    d.list_base = ib + st;
+    d.out_base = base + du + st;
+    d.q = (int32_t)q;
+    d.pos0 = (int32_t)(du + st);
+    d.len = (int32_t)(di - st < kChunk ? di - st : kChunk);
+    d.side = 1;
+    cdesc[c] = d;
   }
 }
 
@@ -274,18 +312,21 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
   return hipGetLastError();
 }
 
-hipError_t build_chunks(fia_ctx* c, int64_t Q, const int64_t* offsets, int64_t max_chunks, hipStream_t s) {
+hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                        int64_t max_chunks, hipStream_t s) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
-  FIA_HIP_TRY(c->cquery.reserve(sizeof(int32_t) * (size_t)(max_chunks + 1)));
-  FIA_HIP_TRY(c->cstart.reserve(sizeof(int32_t) * (size_t)(max_chunks + 1)));
+  FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1)));
   FIA_HIP_TRY(c->nch.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
   int64_t* nch = c->nch.as<int64_t>();
-  hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)((Q + 1 + 255) / 256)), dim3(256), 0, s, offsets, Q, nch);
+  const int64_t* uptr = c->idx.side[0].ptr.as<int64_t>();
+  const int64_t* iptr = c->idx.side[1].ptr.as<int64_t>();
+  hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)((Q + 1 + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr,
+                     c->idx.U, c->idx.I, nch);
   FIA_HIP_TRY(hipGetLastError());
   FIA_HIP_TRY(exclusive_scan_i64(c, nch, c->coff.as<int64_t>(), Q + 1, s));
   if (Q > 0) {
-    hipLaunchKernelGGL(k_chunk_fill, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, c->coff.as<int64_t>(), Q,
-                       c->cquery.as<int32_t>(), c->cstart.as<int32_t>());
+    hipLaunchKernelGGL(k_chunk_fill, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr,
+                       c->idx.U, c->idx.I, offsets, c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>());
     FIA_HIP_TRY(hipGetLastError());
   }
   return hipSuccess;

@@ -60,6 +60,14 @@ struct NCFm {
 
 __device__ __forceinline__ int tri(int r, int c) { return (r * (r + 1)) / 2 + c; }
 
+// lane l's double, broadcast to the wave (v_readlane into SGPRs; l compile-time)
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 template <int N>
 __device__ __forceinline__ void load_row_f32(const float* __restrict__ src, double* dst) {
   if constexpr (N % 4 == 0) {
@@ -790,81 +798,121 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb, const int32
 }
 
 // ------------------------------------------------------------------------------------
-// Scoring: one workgroup per chunk of <= kChunk related ratings of one query.
-// influence = (2 e s + c_q) / n with s = x . g_j (mf:240-246)
+// Scoring (the dominant, HBM-streaming kernel): one WAVE per chunk of <= 64*RW
+// consecutive ratings of one side of one query; the 4 waves of a block are
+// independent (no block barrier after the NCF weight load).  Everything the chunk
+// needs from its query is wave-uniform (scalar loads).  Per rating j:
+//   influence_j = (2 e_j s_j + c_q) / n,  s_j = x . g_j,  e_j = r-hat_j - y_j
+// (mf:240-246: x . grad L_j / n with grad L_j = 2 e_j g_j + wd * M * theta_t).
+// The chunk's K best (|influence| desc, position asc) go to its candidate slots.
 // ------------------------------------------------------------------------------------
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score(
-    QueryArgs A, int64_t Q, const int64_t* __restrict__ offsets, const int64_t* __restrict__ coff,
-    const int32_t* __restrict__ cquery, const int32_t* __restrict__ cstart, const double* __restrict__ rec,
-    int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos,
-    double* __restrict__ cand_val) {
-  constexpr int K = M::K;
-  __shared__ double sr[M::R];
+    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  constexpr int K = M::K, RW = kScoreRows;
   __shared__ NCFWeights<M::ncf ? K : 2> w;
-  __shared__ double s_a[kScoreThreads / 64], s_v[kScoreThreads / 64];
-  __shared__ int s_p[kScoreThreads / 64];
-  const int64_t nchunks = coff[Q];
-  const int tid = threadIdx.x;
   if constexpr (M::ncf) {
     load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
+    __syncthreads();
   }
-  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const int32_t q = cquery[ch];
-    const int32_t start = cstart[ch];
-    const int32_t u = A.qu[q], i = A.qi[q];
-    const int64_t ub = A.ptr[0][u], du = A.ptr[0][u + 1] - ub;
-    const int64_t ib = A.ptr[1][i];
-    const int64_t base = offsets[q];
-    const int64_t n = offsets[q + 1] - base;
-    // list entries first: they do not depend on the query record
-    int32_t o_[kScoreRows], row_[kScoreRows];
-    float y_[kScoreRows];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nchunks = coff[Q];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  for (int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; ch < nchunks; ch += stride) {
+    const ChunkDesc d = cdesc[ch];
+    const int sd = d.side;
+    const int32_t* __restrict__ oth = A.other[sd] + d.list_base;
+    const float* __restrict__ rat = A.rating[sd] + d.list_base;
+    const int32_t* __restrict__ rw = A.row[sd] + d.list_base;
+    // the query record, spread over the lanes (lane c holds word c of this side's
+    // record; read back with v_readlane), loaded together with the list entries
+    const double* __restrict__ R = rec + (int64_t)d.q * M::R;
+    const double* __restrict__ Sg = R + 4 + sd * M::SB;
+    constexpr int NV = (M::SB + 63) / 64;
+    const double hv = R[lane & 3];
+    double rv[NV];
 #pragma unroll
-    for (int rr = 0; rr < kScoreRows; ++rr) {
-      const int64_t p = (int64_t)start + rr * kScoreThreads + tid;
-      o_[rr] = -1;
-      if (p < n) {
-        const int sd = p < du ? 0 : 1;
-        const int64_t li = sd == 0 ? ub + p : ib + (p - du);
-        o_[rr] = A.other[sd][li];
-        y_[rr] = A.rating[sd][li];
-        row_[rr] = A.row[sd][li];
+    for (int v = 0; v < NV; ++v) rv[v] = Sg[v * 64 + lane < M::SB ? v * 64 + lane : M::SB - 1];
+    // list entries (coalesced, branch-free: lanes past the chunk end re-read entry 0),
+    // then every row's gather issued before any arithmetic
+    int32_t o_[RW], row_[RW];
+    float y_[RW];
+    bool ok_[RW];
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int idx = r * 64 + lane;
+      ok_[r] = idx < d.len;
+      const int li = ok_[r] ? idx : 0;
+      o_[r] = oth[li];
+      y_[r] = rat[li];
+      row_[r] = rw[li];
+    }
+    // pin the list loads here: without this hipcc sinks the row-index load into the
+    // (conditional) rel_idx store and serialises one HBM round trip per row
+#pragma unroll
+    for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
+    float4 g4_[M::ncf ? 1 : RW][M::ncf ? 1 : K / 4];
+    float gb_[RW];
+    if constexpr (!M::ncf) {
+      const float* T = sd == 0 ? A.t[1] : A.t[0];
+      const float* bt = sd == 0 ? A.t[3] : A.t[2];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
+#pragma unroll
+        for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
+        gb_[r] = bt[o_[r]];
+      }
+      // all gathers in flight before the first use
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+#pragma unroll
+        for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
+        asm volatile("" ::"v"(gb_[r]));
       }
     }
-    __syncthreads();
-    for (int t = tid; t < M::R; t += kScoreThreads) sr[t] = rec[(int64_t)q * M::R + t];
-    __syncthreads();
-    const double inv_n = sr[0], cq = sr[1], xv = sr[2], rhat_ui = sr[3];
-    double ca[kScoreRows], cv[kScoreRows];
-    int cp[kScoreRows];
+    const double inv_n = readlane_d(hv, 0), cq = readlane_d(hv, 1), xv = readlane_d(hv, 2),
+                 rhat_ui = readlane_d(hv, 3);
+    const double* __restrict__ S = Sg;   // NCF reads its (longer) record directly
+    double ca[RW], cv[RW];
+    int cp[RW];
+    // MF: the two dot products of every row with the record's (p_self, x_self); the
+    // coordinate loop is outermost so each record word is broadcast once per chunk
+    double dot_a[RW], dot_x[RW];
+    if constexpr (!M::ncf) {
+#define RS(c) readlane_d(rv[(c) / 64], (c) % 64)
 #pragma unroll
-    for (int rr = 0; rr < kScoreRows; ++rr) {
-      const int64_t p = (int64_t)start + rr * kScoreThreads + tid;
-      cp[rr] = -1;
-      ca[rr] = -2.0;
-      cv[rr] = 0.0;
-      if (p >= n) continue;
-      const int sd = p < du ? 0 : 1;
-      const int32_t o = o_[rr];
-      const double y = (double)y_[rr];
-      const double* S = sr + 4 + sd * M::SB;
+      for (int r = 0; r < RW; ++r) dot_a[r] = dot_x[r] = 0.0;
+#pragma unroll
+      for (int c4 = 0; c4 < K / 4; ++c4) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          const double ac = RS(4 * c4 + cc), xc = RS(K + 4 * c4 + cc);
+#pragma unroll
+          for (int r = 0; r < RW; ++r) {
+            const float4 t = g4_[r][c4];
+            const double tv = (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w);
+            dot_a[r] = fma(ac, tv, dot_a[r]);
+            dot_x[r] = fma(xc, tv, dot_x[r]);
+          }
+        }
+      }
+    }
+    const double bias_s = M::ncf ? 0.0 : RS(2 * K), xsb = M::ncf ? 0.0 : RS(2 * K + 1);
+    const double dup_o = M::ncf ? 0.0 : RS(2 * K + 2);
+#undef RS
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const int32_t o = o_[r];
+      const double y = (double)y_[r];
       double e, s;
       if constexpr (!M::ncf) {
-        // other-side embedding and bias: side 0 (user rows) -> item tables, side 1 -> user tables
-        const float* T = sd == 0 ? A.t[1] : A.t[0];
-        const float* bt = sd == 0 ? A.t[3] : A.t[2];
-        double row_e[K];
-        load_row_f32<K>(T + (int64_t)o * K, row_e);
-        double dot_a = 0.0, dot_x = 0.0;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-          dot_a = fma(S[c], row_e[c], dot_a);
-          dot_x = fma(S[K + c], row_e[c], dot_x);
-        }
-        e = dot_a + S[2 * K] + (double)bt[o] - y;
-        s = dot_x + S[2 * K + 1];
-        if ((double)o == S[2 * K + 2]) { e = rhat_ui - y; s = xv; }
+        e = dot_a[r] + bias_s + (double)gb_[r] - y;
+        s = dot_x[r] + xsb;
+        if ((double)o == dup_o) { e = rhat_ui - y; s = xv; }
       } else {
         const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o * K;
         const float* G = (sd == 0 ? A.t[3] : A.t[2]) + (int64_t)o * K;   // other side gmf row
@@ -885,15 +933,36 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
         if ((double)o == S[4 * K]) { e = rhat_ui - y; s = xv; }
       }
       const double infl = (2.0 * e * s + cq) * inv_n;
-      if (influence) influence[base + p] = infl;
-      if (rel_idx) rel_idx[base + p] = row_[rr];
-      cp[rr] = (int)p;
-      ca[rr] = topk_key(infl);
-      cv[rr] = infl;
+      const int idx = r * 64 + lane;
+      if (ok_[r]) {
+        if (influence) influence[d.out_base + idx] = infl;
+        if (rel_idx) rel_idx[d.out_base + idx] = row_[r];
+      }
+      cp[r] = ok_[r] ? d.pos0 + idx : -1;
+      ca[r] = ok_[r] ? topk_key(infl) : -2.0;
+      cv[r] = infl;
     }
-    if (K_top > 0)
-      block_topk<kScoreRows, kScoreThreads>(ca, cp, cv, K_top, cand_pos + ch * K_top, cand_val + ch * K_top, s_a, s_p,
-                                            s_v);
+    if (K_top > 0) {
+      double pa = INFINITY;
+      int pp = -1;
+      for (int t = 0; t < K_top; ++t) {
+        double ba = -2.0, bv = 0.0;
+        int bp = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < RW; ++r)
+          if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
+            ba = ca[r]; bp = cp[r]; bv = cv[r];
+          }
+        wave_best(ba, bp, bv);
+        if (lane == 0) {
+          const bool ok = ba > -1.5;
+          cand_pos[ch * K_top + t] = ok ? bp : -1;
+          cand_val[ch * K_top + t] = ok ? bv : NAN;
+        }
+        pa = ba;
+        pp = bp;
+      }
+    }
   }
 }
 
@@ -1025,7 +1094,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   QueryArgs A = make_args(c, qu, qi);
   phase_begin(c, 4, s);
-  FIA_HIP_TRY(build_chunks(c, Q, offsets, max_chunks, s));
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   if constexpr (use_tps<M>()) {
@@ -1043,12 +1112,13 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
-  int64_t grid = max_chunks < 1 ? 1 : max_chunks;
-  if (grid > 16384) grid = 16384;
+  int64_t grid = (max_chunks + 3) / 4;            // 4 waves (chunks) per block
+  if (grid < 1) grid = 1;
+  if (grid > 8192) grid = 8192;
   phase_begin(c, 2, s);
-  hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, offsets,
-                     c->coff.as<int64_t>(), c->cquery.as<int32_t>(), c->cstart.as<int32_t>(), c->rec.as<double>(),
-                     rel_idx, influence, K, c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+  hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(),
+                     c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence, K,
+                     c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);
   if (K > 0 && Q > 0) {

@@ -1,0 +1,65 @@
+"""Multi-process (gloo, world size 2, CPU) tests of the query sharding and the
+final top-K gather -- the only exchange of the multi-GPU path."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from influence.sharding import shard_ranges, gather_topk
+
+
+def test_shard_ranges_balanced_and_contiguous():
+    rng = np.random.default_rng(0)
+    costs = rng.integers(1, 5000, 12074)
+    for ws in (1, 2, 3, 8):
+        rs = shard_ranges(costs, ws)
+        assert len(rs) == ws and rs[0][0] == 0 and rs[-1][1] == costs.size
+        assert all(rs[r][1] == rs[r + 1][0] for r in range(ws - 1))
+        loads = [costs[b:e].sum() for b, e in rs]
+        assert max(loads) <= costs.sum() / ws + costs.max()
+    assert shard_ranges([], 4) == [(0, 0)] * 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, ws, port, qs, K, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        rs = shard_ranges(np.ones(qs), ws)
+        b, e = rs[rank]
+        # stand-in per-rank results: deterministic functions of the global query id
+        q = np.arange(b, e)
+        idx = torch.tensor(np.stack([q * 10 + j for j in range(K)], 1), dtype=torch.int64).reshape(-1, K)
+        val = torch.tensor(np.stack([np.sin(q + j) for j in range(K)], 1), dtype=torch.float64).reshape(-1, K)
+        gi, gv = gather_topk(idx, val)
+        out[rank] = (gi.numpy().copy(), gv.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("qs", [9, 16])
+def test_gather_topk_gloo_world2(qs):
+    K = 3
+    ws = 2
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_worker, args=(ws, _free_port(), qs, K, out), nprocs=ws, join=True)
+        res = dict(out)
+    q = np.arange(qs)
+    want_i = np.stack([q * 10 + j for j in range(K)], 1)
+    want_v = np.stack([np.sin(q + j) for j in range(K)], 1)
+    for r in range(ws):
+        gi, gv = res[r]
+        assert np.array_equal(gi, want_i)
+        assert np.array_equal(gv, want_v)
