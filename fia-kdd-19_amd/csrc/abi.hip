@@ -1,6 +1,7 @@
 // C ABI entry points (include/fia.h).  Validates arguments, keeps the context
 // state machine (params -> index -> prepare -> query), converts HIP errors to
 // status codes + a message, and never lets an exception cross the boundary.
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -82,6 +83,9 @@ int fia_create(int device, fia_ctx** out) {
   fia_ctx* c = new (std::nothrow) fia_ctx();
   if (!c) return FIA_ERR_NOMEM;
   c->device = device;
+  // scoring schedule (A/B knob for profiling): FIA_SCORE=chunk (per-query chunks) or
+  // grouped (entity chunks shared by the batch's queries of that entity)
+  if (const char* m = getenv("FIA_SCORE")) c->score_grouped = std::string(m) == "grouped";
   *out = c;
   return FIA_OK;
 }
@@ -99,10 +103,14 @@ int fia_destroy(fia_ctx* c) {
       c->gram[s].release();
       c->l1[s].release();
       c->idx.order[s].release();
+      c->idx.gitems[s].release();
+      c->idx.gcomb[s].release();
+      c->gpart[s].release();
     }
-    fia::DevBuf* bufs[] = {&c->rec,      &c->coff,     &c->cdesc,                &c->cand_pos,  &c->cand_val,
-                           &c->scan_tmp, &c->flag,     &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt,
-                           &c->idx.psum};
+    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->scan_tmp,
+                           &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
+                           &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->wcnt,
+                           &c->wstart, &c->witems};
     for (auto* b : bufs) b->release();
     for (auto& v : c->events.ev)
       for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }

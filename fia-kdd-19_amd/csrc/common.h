@@ -29,6 +29,7 @@ struct ChunkDesc {
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 512;          // list rows per Gram work item
+constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item
 
 // Device buffer with grow-on-demand capacity (never shrinks).
 struct DevBuf {
@@ -151,6 +152,17 @@ struct fia_ctx {
   fia::DevBuf flag;       // int32 [4] device status words
   fia::DevBuf nch;        // int64 [Q+1] chunk counts
   fia::DevBuf coupled;    // int32 [Q + 1]: count, then queries whose test pair is a train row
+  // query groups per entity (entity-shared scoring): global entity index g = e (users) or
+  // U + e (items)
+  fia::DevBuf gcnt;       // int64 [U + I + 1] queries per entity -> exclusive scan in gstart
+  fia::DevBuf gstart;     // int64 [U + I + 1]
+  fia::DevBuf grank;      // int32 [2Q] rank of query q in its user group / item group
+  fia::DevBuf gq;         // int32 [2Q] queries grouped by entity (users then items)
+  fia::DevBuf qbase;      // int64 [2Q] per query and side: output base, candidate-slot base
+  fia::DevBuf wcnt;       // int64 [U + I + 1] work items per entity -> scan in wstart
+  fia::DevBuf wstart;     // int64 [U + I + 1]
+  fia::DevBuf witems;     // int32 [3 * max items] {global entity, list chunk, query block}
+  bool score_grouped = false;   // scoring schedule, see fia_create
   bool profiling = false;
   fia::PhaseEvents events;
 };
@@ -164,9 +176,13 @@ hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
                          int64_t* offsets, hipStream_t s);
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
                          const int64_t* offsets, int64_t* rel, hipStream_t s);
+// per-query chunk offsets coff (+ chunk descriptors unless offsets_only)
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, hipStream_t s);
+                        int64_t max_chunks, bool offsets_only, hipStream_t s);
 hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
+// per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
+hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                        int64_t max_items, hipStream_t s);
 
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported);

@@ -146,6 +146,62 @@ __global__ void k_chunk_fill(const int32_t* __restrict__ qu, const int32_t* __re
   }
 }
 
+// ---- query groups (entity-shared scoring) ----
+// thread per query: rank inside its user group and its item group; per side the output
+// base (offsets[q], offsets[q] + |R_u|) and candidate-slot base (coff[q], coff[q] + chunks of R_u)
+__global__ void k_group_count(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
+                              const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
+                              const int64_t* __restrict__ offsets, const int64_t* __restrict__ coff,
+                              unsigned long long* __restrict__ gcnt, int32_t* __restrict__ grank,
+                              int64_t* __restrict__ qbase) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  int64_t ub, du, ib, di;
+  query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
+  const int32_t u = qu[q], i = qi[q];
+  const bool ok = (u >= 0 && u < U && i >= 0 && i < I) && (du + di > 0);
+  grank[2 * q] = ok ? (int32_t)atomicAdd(&gcnt[u], 1ull) : -1;
+  grank[2 * q + 1] = ok ? (int32_t)atomicAdd(&gcnt[U + i], 1ull) : -1;
+  qbase[4 * q + 0] = offsets[q];
+  qbase[4 * q + 1] = offsets[q] + du;
+  qbase[4 * q + 2] = coff[q];
+  qbase[4 * q + 3] = coff[q] + (du + kChunk - 1) / kChunk;
+}
+
+// threads over max(Q, U + I + 1): place queries into their groups; work items per entity
+__global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
+                             const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
+                             const int64_t* __restrict__ gstart, const int32_t* __restrict__ grank,
+                             const unsigned long long* __restrict__ gcnt, int32_t* __restrict__ gq,
+                             int64_t* __restrict__ wcnt) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < Q && grank[2 * t] >= 0) {
+    const int32_t u = qu[t], i = qi[t];
+    gq[gstart[u] + grank[2 * t]] = (int32_t)t;
+    gq[gstart[U + i] + grank[2 * t + 1]] = (int32_t)t;
+  }
+  const int64_t nE = U + I;
+  if (t < nE) {
+    const int64_t deg = t < U ? uptr[t + 1] - uptr[t] : iptr[t - U + 1] - iptr[t - U];
+    wcnt[t] = gcnt[t] > 0 ? ((deg + kChunk - 1) / kChunk) * (((int64_t)gcnt[t] + kQueryBlock - 1) / kQueryBlock) : 0;
+  } else if (t == nE) {
+    wcnt[nE] = 0;
+  }
+}
+
+__global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned long long* __restrict__ gcnt,
+                            int64_t nE, int32_t* __restrict__ witems) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nE) return;
+  const int64_t b = wstart[t], e = wstart[t + 1];
+  const int64_t nqb = ((int64_t)gcnt[t] + kQueryBlock - 1) / kQueryBlock;
+  for (int64_t w = b; w < e; ++w) {
+    witems[3 * w] = (int32_t)t;
+    witems[3 * w + 1] = (int32_t)((w - b) / nqb);    // chunk of the entity's list
+    witems[3 * w + 2] = (int32_t)((w - b) % nqb);    // block of the entity's query group
+  }
+}
+
 // one workgroup per query: rel[offsets[q] + p] = R_u[p] (p < deg u), then C_i
 __global__ void k_write_related(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi,
                                 const int64_t* __restrict__ offsets, const int64_t* __restrict__ uptr,
@@ -313,9 +369,9 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 }
 
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, hipStream_t s) {
+                        int64_t max_chunks, bool offsets_only, hipStream_t s) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
-  FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1)));
+  if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1)));
   FIA_HIP_TRY(c->nch.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
   int64_t* nch = c->nch.as<int64_t>();
   const int64_t* uptr = c->idx.side[0].ptr.as<int64_t>();
@@ -324,12 +380,44 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                      c->idx.U, c->idx.I, nch);
   FIA_HIP_TRY(hipGetLastError());
   FIA_HIP_TRY(exclusive_scan_i64(c, nch, c->coff.as<int64_t>(), Q + 1, s));
-  if (Q > 0) {
+  if (Q > 0 && !offsets_only) {
     hipLaunchKernelGGL(k_chunk_fill, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr,
                        c->idx.U, c->idx.I, offsets, c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>());
     FIA_HIP_TRY(hipGetLastError());
   }
   return hipSuccess;
+}
+
+hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                        int64_t max_items, hipStream_t s) {
+  const int64_t U = c->idx.U, I = c->idx.I, nE = U + I;
+  FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
+  FIA_HIP_TRY(c->gstart.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
+  FIA_HIP_TRY(c->wcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
+  FIA_HIP_TRY(c->wstart.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
+  FIA_HIP_TRY(c->grank.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1)));
+  FIA_HIP_TRY(c->gq.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1)));
+  FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1)));
+  FIA_HIP_TRY(c->witems.reserve(sizeof(int32_t) * (size_t)(3 * max_items + 3)));
+  const int64_t* uptr = c->idx.side[0].ptr.as<int64_t>();
+  const int64_t* iptr = c->idx.side[1].ptr.as<int64_t>();
+  FIA_HIP_TRY(hipMemsetAsync(c->gcnt.ptr, 0, sizeof(int64_t) * (size_t)(nE + 1), s));
+  if (Q > 0) {
+    hipLaunchKernelGGL(k_group_count, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr, U, I,
+                       offsets, c->coff.as<int64_t>(), c->gcnt.as<unsigned long long>(), c->grank.as<int32_t>(),
+                       c->qbase.as<int64_t>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  FIA_HIP_TRY(exclusive_scan_i64(c, c->gcnt.as<int64_t>(), c->gstart.as<int64_t>(), nE + 1, s));
+  const int64_t nt = (Q > nE + 1 ? Q : nE + 1);
+  hipLaunchKernelGGL(k_group_fill, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr, U, I,
+                     c->gstart.as<int64_t>(), c->grank.as<int32_t>(), c->gcnt.as<unsigned long long>(),
+                     c->gq.as<int32_t>(), c->wcnt.as<int64_t>());
+  FIA_HIP_TRY(hipGetLastError());
+  FIA_HIP_TRY(exclusive_scan_i64(c, c->wcnt.as<int64_t>(), c->wstart.as<int64_t>(), nE + 1, s));
+  hipLaunchKernelGGL(k_item_fill, dim3((unsigned)((nE + 255) / 256)), dim3(256), 0, s, c->wstart.as<int64_t>(),
+                     c->gcnt.as<unsigned long long>(), nE, c->witems.as<int32_t>());
+  return hipGetLastError();
 }
 
 }  // namespace fia

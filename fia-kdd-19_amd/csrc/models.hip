@@ -187,6 +187,40 @@ __device__ __forceinline__ double ncf_mlp(const NCFWeights<K>& w, const double (
   return mlp;
 }
 
+// Same MLP, but instead of materialising d1 returns yv . d1 (the scoring kernel's only
+// use of it), one hidden unit at a time: 1.5k live doubles fewer per row.
+template <int K>
+__device__ __forceinline__ double ncf_mlp_dot(const NCFWeights<K>& w, const double (&z1)[K],
+                                              const double* __restrict__ yv, double& yd1) {
+  constexpr int H = K / 2;
+  double z2[H];
+#pragma unroll
+  for (int d = 0; d < H; ++d) z2[d] = w.b2[d];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const double h = z1[c] > 0.0 ? z1[c] : 0.0;
+#pragma unroll
+    for (int d = 0; d < H; ++d) z2[d] = fma(w.W2[c * H + d], h, z2[d]);
+  }
+  double mlp = 0.0;
+#pragma unroll
+  for (int d = 0; d < H; ++d) {
+    const bool on = z2[d] > 0.0;
+    mlp = fma(w.W3[d], on ? z2[d] : 0.0, mlp);
+    z2[d] = on ? w.W3[d] : 0.0;                 // z2 now holds d2
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    double t = 0.0;
+#pragma unroll
+    for (int d = 0; d < H; ++d) t = fma(w.W2[c * H + d], z2[d], t);
+    if (z1[c] > 0.0) acc = fma(yv[c], t, acc);
+  }
+  yd1 = acc;
+  return mlp;
+}
+
 template <int K>
 __device__ void load_ncf_weights(NCFWeights<K>& w, const float* W2, const float* b2, const float* W3) {
   constexpr int H = K / 2;
@@ -811,7 +845,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
     QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  constexpr int K = M::K, RW = kScoreRows;
+  constexpr int K = M::K;
+  constexpr int RT = kScoreRows;                 // rows per lane per chunk
+  constexpr int RW = M::ncf ? 4 : kScoreRows;    // rows per lane per pass (NCF: register budget)
+  constexpr int NPASS = RT / RW;
   __shared__ NCFWeights<M::ncf ? K : 2> w;
   if constexpr (M::ncf) {
     load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
@@ -836,111 +873,114 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
     double rv[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) rv[v] = Sg[v * 64 + lane < M::SB ? v * 64 + lane : M::SB - 1];
-    // list entries (coalesced, branch-free: lanes past the chunk end re-read entry 0),
-    // then every row's gather issued before any arithmetic
-    int32_t o_[RW], row_[RW];
-    float y_[RW];
-    bool ok_[RW];
+    double ca[RT], cv[RT];
+    int cp[RT];
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      const int idx = r * 64 + lane;
-      ok_[r] = idx < d.len;
-      const int li = ok_[r] ? idx : 0;
-      o_[r] = oth[li];
-      y_[r] = rat[li];
-      row_[r] = rw[li];
-    }
-    // pin the list loads here: without this hipcc sinks the row-index load into the
-    // (conditional) rel_idx store and serialises one HBM round trip per row
-#pragma unroll
-    for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
-    float4 g4_[M::ncf ? 1 : RW][M::ncf ? 1 : K / 4];
-    float gb_[RW];
-    if constexpr (!M::ncf) {
-      const float* T = sd == 0 ? A.t[1] : A.t[0];
-      const float* bt = sd == 0 ? A.t[3] : A.t[2];
-#pragma unroll
+    for (int h = 0; h < NPASS; ++h) {
+      // list entries (coalesced, branch-free: lanes past the chunk end re-read entry 0),
+      // then every row's gather issued before any arithmetic
+      int32_t o_[RW], row_[RW];
+      float y_[RW];
+      bool ok_[RW];
+  #pragma unroll
       for (int r = 0; r < RW; ++r) {
-        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
-#pragma unroll
-        for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
-        gb_[r] = bt[o_[r]];
+        const int idx = (h * RW + r) * 64 + lane;
+        ok_[r] = idx < d.len;
+        const int li = ok_[r] ? idx : 0;
+        o_[r] = oth[li];
+        y_[r] = rat[li];
+        row_[r] = rw[li];
       }
-      // all gathers in flight before the first use
-#pragma unroll
-      for (int r = 0; r < RW; ++r) {
-#pragma unroll
-        for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
-        asm volatile("" ::"v"(gb_[r]));
+      // pin the list loads here: without this hipcc sinks the row-index load into the
+      // (conditional) rel_idx store and serialises one HBM round trip per row
+  #pragma unroll
+      for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
+      float4 g4_[M::ncf ? 1 : RW][M::ncf ? 1 : K / 4];
+      float gb_[RW];
+      if constexpr (!M::ncf) {
+        const float* T = sd == 0 ? A.t[1] : A.t[0];
+        const float* bt = sd == 0 ? A.t[3] : A.t[2];
+  #pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
+  #pragma unroll
+          for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
+          gb_[r] = bt[o_[r]];
+        }
+        // all gathers in flight before the first use
+  #pragma unroll
+        for (int r = 0; r < RW; ++r) {
+  #pragma unroll
+          for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
+          asm volatile("" ::"v"(gb_[r]));
+        }
       }
-    }
-    const double inv_n = readlane_d(hv, 0), cq = readlane_d(hv, 1), xv = readlane_d(hv, 2),
-                 rhat_ui = readlane_d(hv, 3);
-    const double* __restrict__ S = Sg;   // NCF reads its (longer) record directly
-    double ca[RW], cv[RW];
-    int cp[RW];
-    // MF: the two dot products of every row with the record's (p_self, x_self); the
-    // coordinate loop is outermost so each record word is broadcast once per chunk
-    double dot_a[RW], dot_x[RW];
-    if constexpr (!M::ncf) {
-#define RS(c) readlane_d(rv[(c) / 64], (c) % 64)
-#pragma unroll
-      for (int r = 0; r < RW; ++r) dot_a[r] = dot_x[r] = 0.0;
-#pragma unroll
-      for (int c4 = 0; c4 < K / 4; ++c4) {
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          const double ac = RS(4 * c4 + cc), xc = RS(K + 4 * c4 + cc);
-#pragma unroll
-          for (int r = 0; r < RW; ++r) {
-            const float4 t = g4_[r][c4];
-            const double tv = (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w);
-            dot_a[r] = fma(ac, tv, dot_a[r]);
-            dot_x[r] = fma(xc, tv, dot_x[r]);
+      const double inv_n = readlane_d(hv, 0), cq = readlane_d(hv, 1), xv = readlane_d(hv, 2),
+                   rhat_ui = readlane_d(hv, 3);
+      const double* __restrict__ S = Sg;   // NCF reads its (longer) record directly
+      // MF: the two dot products of every row with the record's (p_self, x_self); the
+      // coordinate loop is outermost so each record word is broadcast once per chunk
+      double dot_a[RW], dot_x[RW];
+      if constexpr (!M::ncf) {
+  #define RS(c) readlane_d(rv[(c) / 64], (c) % 64)
+  #pragma unroll
+        for (int r = 0; r < RW; ++r) dot_a[r] = dot_x[r] = 0.0;
+  #pragma unroll
+        for (int c4 = 0; c4 < K / 4; ++c4) {
+  #pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const double ac = RS(4 * c4 + cc), xc = RS(K + 4 * c4 + cc);
+  #pragma unroll
+            for (int r = 0; r < RW; ++r) {
+              const float4 t = g4_[r][c4];
+              const double tv = (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w);
+              dot_a[r] = fma(ac, tv, dot_a[r]);
+              dot_x[r] = fma(xc, tv, dot_x[r]);
+            }
           }
         }
       }
-    }
-    const double bias_s = M::ncf ? 0.0 : RS(2 * K), xsb = M::ncf ? 0.0 : RS(2 * K + 1);
-    const double dup_o = M::ncf ? 0.0 : RS(2 * K + 2);
-#undef RS
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      const int32_t o = o_[r];
-      const double y = (double)y_[r];
-      double e, s;
-      if constexpr (!M::ncf) {
-        e = dot_a[r] + bias_s + (double)gb_[r] - y;
-        s = dot_x[r] + xsb;
-        if ((double)o == dup_o) { e = rhat_ui - y; s = xv; }
-      } else {
-        const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o * K;
-        const float* G = (sd == 0 ? A.t[3] : A.t[2]) + (int64_t)o * K;   // other side gmf row
-        double z1[K], d1[K], grow[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c) z1[c] = S[c] + L1o[c];
-        const double mlp = ncf_mlp<K>(w, z1, d1);
-        load_row_f32<K>(G, grow);
-        double gmf = 0.0;
-        s = 0.0;
-#pragma unroll
-        for (int c = 0; c < K; ++c) {
-          s = fma(S[K + c], d1[c], s);
-          s = fma(S[2 * K + c], grow[c], s);
-          gmf = fma(S[3 * K + c], grow[c], gmf);
+      const double bias_s = M::ncf ? 0.0 : RS(2 * K), xsb = M::ncf ? 0.0 : RS(2 * K + 1);
+      const double dup_o = M::ncf ? 0.0 : RS(2 * K + 2);
+  #undef RS
+  #pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int32_t o = o_[r];
+        const double y = (double)y_[r];
+        double e, s;
+        if constexpr (!M::ncf) {
+          e = dot_a[r] + bias_s + (double)gb_[r] - y;
+          s = dot_x[r] + xsb;
+          if ((double)o == dup_o) { e = rhat_ui - y; s = xv; }
+        } else {
+          const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o * K;
+          const float* G = (sd == 0 ? A.t[3] : A.t[2]) + (int64_t)o * K;   // other side gmf row
+          double z1[K];
+  #pragma unroll
+          for (int c = 0; c < K; ++c) z1[c] = S[c] + L1o[c];
+          double yd1;
+          const double mlp = ncf_mlp_dot<K>(w, z1, S + K, yd1);   // yd1 = yv . d1
+          double gmf = 0.0;
+          s = yd1;
+  #pragma unroll
+          for (int c = 0; c < K; ++c) {
+            const double g = (double)G[c];
+            s = fma(S[2 * K + c], g, s);
+            gmf = fma(S[3 * K + c], g, gmf);
+          }
+          e = mlp + gmf + (double)A.t[9][0] - y;
+          if ((double)o == S[4 * K]) { e = rhat_ui - y; s = xv; }
         }
-        e = mlp + gmf + (double)A.t[9][0] - y;
-        if ((double)o == S[4 * K]) { e = rhat_ui - y; s = xv; }
+        const double infl = (2.0 * e * s + cq) * inv_n;
+        const int idx = (h * RW + r) * 64 + lane;
+        if (ok_[r]) {   // streaming outputs: nontemporal, so they do not evict the gathered tables from L2
+          if (influence) __builtin_nontemporal_store(infl, influence + d.out_base + idx);
+          if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + d.out_base + idx);
+        }
+        cp[h * RW + r] = ok_[r] ? d.pos0 + idx : -1;
+        ca[h * RW + r] = ok_[r] ? topk_key(infl) : -2.0;
+        cv[h * RW + r] = infl;
       }
-      const double infl = (2.0 * e * s + cq) * inv_n;
-      const int idx = r * 64 + lane;
-      if (ok_[r]) {
-        if (influence) influence[d.out_base + idx] = infl;
-        if (rel_idx) rel_idx[d.out_base + idx] = row_[r];
-      }
-      cp[r] = ok_[r] ? d.pos0 + idx : -1;
-      ca[r] = ok_[r] ? topk_key(infl) : -2.0;
-      cv[r] = infl;
     }
     if (K_top > 0) {
       double pa = INFINITY;
@@ -949,7 +989,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
         double ba = -2.0, bv = 0.0;
         int bp = 0x7fffffff;
 #pragma unroll
-        for (int r = 0; r < RW; ++r)
+        for (int r = 0; r < RT; ++r)
           if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
             ba = ca[r]; bp = cp[r]; bv = cv[r];
           }
@@ -966,9 +1006,273 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Entity-shared scoring.  A work item is one chunk (<= kChunk ratings) of ONE entity's
+// list (user list R_u or item list C_i) together with every query of the batch that
+// has that entity.  The list entries, the gathered other-side embedding rows and the
+// per-rating residual e_j = r-hat_j - y_j (and, for NCF, the MLP backward vector
+// d1_j) depend on the train rating only, so they are loaded / computed once per work
+// item and reused for every query in the group; per query only s_jq = x_q . g_j is
+// new.  influence_jq = (2 e_j s_jq + c_q) / n_q  (mf:240-246).  The test pair's own
+// train row takes e and s from the query record (bit-identical copies, see k_solve).
+// ------------------------------------------------------------------------------------
+// rows per lane per scoring pass (register budget of the gathered rows / NCF backward
+// vectors); kScoreRows / score_rw passes per work item, one candidate slot set each
+template <class M>
+constexpr int score_rw() {
+  return M::ncf ? (M::K >= 32 ? 1 : 2) : (M::K >= 64 ? 1 : M::K >= 32 ? 2 : 4);
+}
+
+template <class M>
+__global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
+    QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
+    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  constexpr int K = M::K;
+  constexpr int RT = kScoreRows;                 // rows per lane per work item
+  constexpr int RW = score_rw<M>();              // rows per lane per pass
+  constexpr int NPASS = RT / RW;
+  constexpr int NSV = (K + 1 + 63) / 64;         // entity words per lane
+  constexpr int QB = kQueryBlock;
+  constexpr int RSW = 4 + M::SB;                  // staged record words: header + this side's block
+  __shared__ NCFWeights<M::ncf ? K : 2> w;
+  // per wave: the query block's records (uniform-address reads = LDS broadcasts) and
+  // per query {output base, candidate-slot base, position offset}
+  __shared__ double srec[kScoreThreads / 64][QB * RSW];
+  __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
+  if constexpr (M::ncf) {
+    load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_items = wstart[nE];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
+    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int sd = g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(g - A.U) : g;
+    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
+    const int64_t gn = gstart[g + 1] - gb;
+    const int nq = gn < QB ? (int)gn : QB;
+    const int32_t* __restrict__ oth = A.other[sd] + lb;
+    const float* __restrict__ rat = A.rating[sd] + lb;
+    const int32_t* __restrict__ rw = A.row[sd] + lb;
+    // the entity's own parameters, spread over lanes (MF: embedding + bias; NCF: its
+    // layer-1 half + b1)
+    double selfv[NSV];
+#pragma unroll
+    for (int v = 0; v < NSV; ++v) {
+      const int c = v * 64 + lane;
+      if constexpr (!M::ncf) {
+        const float* Es = sd == 0 ? A.t[0] : A.t[1];
+        const float* Bs = sd == 0 ? A.t[2] : A.t[3];
+        selfv[v] = c < K ? (double)Es[(int64_t)e * K + c] : (double)Bs[e];
+      } else {
+        selfv[v] = c < K ? A.l1[sd][(int64_t)e * K + c] + (double)A.t[5][c] : 0.0;
+      }
+    }
+#define SV(c) readlane_d(selfv[(c) / 64], (c) % 64)
+    // stage the query block (queries past the group end repeat the last one; never used)
+    double* __restrict__ rl = srec[wave];
+    int64_t* __restrict__ bl = sbase[wave];
+    __builtin_amdgcn_wave_barrier();
+    for (int t = lane; t < QB * RSW; t += 64) {
+      const int j = t / RSW, c = t - j * RSW;
+      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
+      rl[t] = rec[(int64_t)q * M::R + (c < 4 ? c : 4 + sd * M::SB + (c - 4))];
+    }
+    if (lane < QB) {
+      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
+      const int64_t* qb = qbase + 4 * (int64_t)q;
+      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
+      bl[QB + lane] = qb[2 + sd] + cidx;
+      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < NPASS; ++h) {
+      int32_t o_[RW], row_[RW];
+      float y_[RW];
+      bool ok_[RW];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        const int idx = (h * RW + r) * 64 + lane;
+        ok_[r] = idx < len;
+        const int li = ok_[r] ? idx : 0;
+        o_[r] = oth[li];
+        y_[r] = rat[li];
+        row_[r] = rw[li];
+      }
+#pragma unroll
+      for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
+      // per-rating quantities shared by the whole query block
+      float4 g4_[RW][(K + 3) / 4];               // other-side embedding row (MF: dot with x; NCF: gmf row)
+      double ej[RW];                             // residual r-hat_j - y_j
+      double d1_[M::ncf ? RW : 1][M::ncf ? K : 1];   // NCF: masked backward vector
+      {
+        const float* T = sd == 0 ? (M::ncf ? A.t[3] : A.t[1]) : (M::ncf ? A.t[2] : A.t[0]);
+        float gb_[RW];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
+#pragma unroll
+          for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
+          if constexpr (!M::ncf) gb_[r] = (sd == 0 ? A.t[3] : A.t[2])[o_[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+#pragma unroll
+          for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
+        }
+        if constexpr (!M::ncf) {
+          const double gbias = (double)A.t[4][0];
+          const double bself = SV(K);
+#pragma unroll
+          for (int r = 0; r < RW; ++r) ej[r] = 0.0;
+#pragma unroll
+          for (int c4 = 0; c4 < K / 4; ++c4)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+              const double pc = SV(4 * c4 + cc);
+#pragma unroll
+              for (int r = 0; r < RW; ++r) {
+                const float4 t = g4_[r][c4];
+                ej[r] = fma(pc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), ej[r]);
+              }
+            }
+#pragma unroll
+          for (int r = 0; r < RW; ++r) ej[r] = ej[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
+        } else {
+          const double b3 = (double)A.t[9][0];
+          const float* Gs = (sd == 0 ? A.t[2] : A.t[3]) + (int64_t)e * K;   // own gmf row
+          const float* W3g = A.t[8] + K / 2;
+#pragma unroll
+          for (int r = 0; r < RW; ++r) {
+            const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o_[r] * K;
+            double z1[K];
+#pragma unroll
+            for (int c = 0; c < K; ++c) z1[c] = SV(c) + L1o[c];
+            const double mlp = ncf_mlp<K>(w, z1, d1_[r]);
+            double gmf = 0.0;
+#pragma unroll
+            for (int c4 = 0; c4 < K / 4; ++c4) {
+              const float4 t = g4_[r][c4];
+              gmf = fma((double)W3g[4 * c4 + 0] * (double)Gs[4 * c4 + 0], (double)t.x, gmf);
+              gmf = fma((double)W3g[4 * c4 + 1] * (double)Gs[4 * c4 + 1], (double)t.y, gmf);
+              gmf = fma((double)W3g[4 * c4 + 2] * (double)Gs[4 * c4 + 2], (double)t.z, gmf);
+              gmf = fma((double)W3g[4 * c4 + 3] * (double)Gs[4 * c4 + 3], (double)t.w, gmf);
+            }
+            ej[r] = mlp + gmf + b3 - (double)y_[r];
+          }
+        }
+      }
+      // every query of the block: s_jq = x_q . g_j, then influence, outputs, candidates
+#pragma unroll 1
+      for (int j = 0; j < nq; ++j) {
+        const double* __restrict__ Rj = rl + j * RSW;
+#define RS(cc) Rj[4 + (cc)]
+        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
+        const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
+        double sj[RW];
+        double dup_o;
+        if constexpr (!M::ncf) {
+#pragma unroll
+          for (int r = 0; r < RW; ++r) sj[r] = 0.0;
+#pragma unroll
+          for (int c4 = 0; c4 < K / 4; ++c4)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+              const double xc = RS(K + 4 * c4 + cc);
+#pragma unroll
+              for (int r = 0; r < RW; ++r) {
+                const float4 t = g4_[r][c4];
+                sj[r] = fma(xc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), sj[r]);
+              }
+            }
+          const double xsb = RS(2 * K + 1);
+#pragma unroll
+          for (int r = 0; r < RW; ++r) sj[r] += xsb;
+          dup_o = RS(2 * K + 2);
+        } else {
+#pragma unroll
+          for (int r = 0; r < RW; ++r) sj[r] = 0.0;
+#pragma unroll
+          for (int c = 0; c < K; ++c) {
+            const double yc = RS(K + c);
+#pragma unroll
+            for (int r = 0; r < RW; ++r) sj[r] = fma(yc, d1_[r][c], sj[r]);
+          }
+#pragma unroll
+          for (int c4 = 0; c4 < K / 4; ++c4)
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+              const double bc = RS(2 * K + 4 * c4 + cc);
+#pragma unroll
+              for (int r = 0; r < RW; ++r) {
+                const float4 t = g4_[r][c4];
+                sj[r] = fma(bc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), sj[r]);
+              }
+            }
+          dup_o = RS(4 * K);
+        }
+#undef RS
+        double la[RW], lv[RW];
+        int lp[RW];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          double ee = ej[r], ss = sj[r];
+          if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
+          const double infl = (2.0 * ee * ss + cq) * inv_n;
+          const int idx = (h * RW + r) * 64 + lane;
+          if (ok_[r]) {   // streaming outputs: nontemporal, so they do not evict the gathered tables from L2
+            if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
+            if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+          }
+          lp[r] = ok_[r] ? cidx * kChunk + idx : -1;    // related position inside this side's list
+          la[r] = ok_[r] ? topk_key(infl) : -2.0;
+          lv[r] = infl;
+        }
+        if (K_top > 0) {
+          // pass h's candidates for this query; k_topk_merge merges the NPASS slot sets of
+          // every chunk: slot (chunk c, pass h) -> c * NPASS + h
+          double pa = INFINITY;
+          int pp = -1;
+          for (int t = 0; t < K_top; ++t) {
+            double ba = -2.0, bv = 0.0;
+            int bp = 0x7fffffff;
+#pragma unroll
+            for (int r = 0; r < RW; ++r)
+              if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
+                ba = la[r]; bp = lp[r]; bv = lv[r];
+              }
+            wave_best(ba, bp, bv);
+            if (lane == 0) {
+              const bool okk = ba > -1.5;
+              const int64_t slot = (cbj * NPASS + h) * K_top + t;
+              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+              cand_val[slot] = okk ? bv : NAN;
+            }
+            pa = ba;
+            pp = bp;
+          }
+        }
+      }
+    }
+#undef SV
+    __builtin_amdgcn_wave_barrier();   // staged block fully consumed before the next item overwrites it
+  }
+}
+
 // Merge the chunk candidates of every query (one wave per query).
 __global__ __launch_bounds__(64) void k_topk_merge(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi,
-                                                   int64_t Q, const int64_t* __restrict__ coff, int K,
+                                                   int64_t Q, const int64_t* __restrict__ coff, int K, int spc,
                                                    const int32_t* __restrict__ cand_pos,
                                                    const double* __restrict__ cand_val,
                                                    const int64_t* __restrict__ uptr, const int32_t* __restrict__ urow,
@@ -978,7 +1282,7 @@ __global__ __launch_bounds__(64) void k_topk_merge(const int32_t* __restrict__ q
   const int64_t q = blockIdx.x;
   if (q >= Q) return;
   const int lane = threadIdx.x;
-  const int64_t cb = coff[q] * K, ce = coff[q + 1] * K;
+  const int64_t cb = coff[q] * spc * K, ce = coff[q + 1] * spc * K;
   const int32_t u = qu[q], i = qi[q];
   const bool ok_id = (u >= 0 && u < U && i >= 0 && i < I);
   const int64_t ub = ok_id ? uptr[u] : 0, du = ok_id ? uptr[u + 1] - ub : 0, ib = ok_id ? iptr[i] : 0;
@@ -1087,14 +1391,21 @@ template <class M>
 hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                       int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+  const bool grouped = c->score_grouped;
+  // candidate slot sets per chunk: k_score_grouped writes one per pass
+  const int spc = grouped ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));
   if (K > 0) {
-    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K)));
-    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K)));
+    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc)));
+    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * spc)));
   }
   QueryArgs A = make_args(c, qu, qi);
+  const int64_t nE = c->idx.U + c->idx.I;
+  // every (entity chunk, query block) item covers >= 1 per-query chunk
+  const int64_t max_items = max_chunks;
   phase_begin(c, 4, s);
-  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, s));
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   if constexpr (use_tps<M>()) {
@@ -1112,18 +1423,25 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
-  int64_t grid = (max_chunks + 3) / 4;            // 4 waves (chunks) per block
+  int64_t grid = (max_items + 3) / 4;            // 4 waves (work items) per block
   if (grid < 1) grid = 1;
   if (grid > 8192) grid = 8192;
   phase_begin(c, 2, s);
-  hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(),
-                     c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence, K,
-                     c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+  if (grouped) {
+    hipLaunchKernelGGL(k_score_grouped<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                       c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
+                       c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
+                       c->cand_val.as<double>());
+  } else {
+    hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(),
+                       c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence, K,
+                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+  }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);
   if (K > 0 && Q > 0) {
     phase_begin(c, 3, s);
-    hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)Q), dim3(64), 0, s, qu, qi, Q, c->coff.as<int64_t>(), K,
+    hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)Q), dim3(64), 0, s, qu, qi, Q, c->coff.as<int64_t>(), K, spc,
                        c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), c->idx.side[0].ptr.as<int64_t>(),
                        c->idx.side[0].row.as<int32_t>(), c->idx.side[1].ptr.as<int64_t>(),
                        c->idx.side[1].row.as<int32_t>(), c->p.U, c->p.I, topk_pos, topk_idx, topk_val);

@@ -219,6 +219,38 @@ def test_yelp_ncf_sample_matches_oracle(tmp_path):
         check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], 2)
 
 
+@pytest.mark.parametrize("model,k", [("MF", 8), ("MF", 16), ("MF", 32), ("MF", 64), ("NCF", 8), ("NCF", 16),
+                                     ("NCF", 32)])
+def test_every_built_size_matches_oracle(model, k, tmp_path):
+    """Every (model, k) the library is built for, on a small random problem with
+    long lists (Gram work items split and recombined), a held-out pair, the pair
+    itself in train and an empty side."""
+    from oracle import fia_oracle as fo
+    rng = np.random.default_rng(k + (100 if model == "NCF" else 0))
+    U, I, N = 700, 30, 3000
+    key = np.sort(rng.choice((U - 1) * I, N - 1, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    # one very long item list: item 0 rated by every user (forces split Gram items at 512/list)
+    extra_u = np.arange(U - 1, dtype=np.int32)
+    tu = np.concatenate([tu, extra_u, [tu[5]]]).astype(np.int32)
+    ti = np.concatenate([ti, np.full(U - 1, I - 1, np.int32), [ti[5]]]).astype(np.int32)
+    tr = rng.integers(1, 6, tu.size).astype(np.float32)
+    p = synth.mf_params(U, I, k, 3) if model == "MF" else synth.ncf_params(U, I, k, 3)
+    qs = [(1, 2), (int(tu[5]), int(ti[5])), (U - 1, 3), (7, I - 1), (int(tu[50]), int(ti[50]))]
+    qu = np.array([q[0] for q in qs], np.int32)
+    qi = np.array([q[1] for q in qs], np.int32)
+    m = make_model(model, U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    res = m.get_influence_batch(list(range(len(qs))), K=3)
+    for q, (u, i) in enumerate(qs):
+        o = fo.query(model, p, k, tu, ti, tr, u, i, 1e-3, 1e-6)
+        b, e = res["offsets"][q], res["offsets"][q + 1]
+        assert np.array_equal(o["rel"], res["rel_idx"][b:e])
+        if o["n"]:
+            assert rel_err(res["influence"][b:e], o["influence"]) < RTOL, (model, k, q)
+            assert rel_err(res["x"][q], o["x"]) < RTOL, (model, k, q)
+            check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], 3)
+
+
 def test_invalid_queries_raise(tmp_path):
     from influence._lib import FIAError
     f = load("small_mf_k16.npz")

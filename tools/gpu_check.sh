@@ -2,7 +2,7 @@
 # One GPU-box session: gpu tests, smoke, bench (+ optional rocprof), each step
 # under its own time limit.  Stops at the first timeout / abort / crash; test
 # failures (exit 1) are recorded and the remaining steps still run.
-# usage: tools/gpu_check.sh [tests|smoke|bench|prof|pmc ...]
+# usage: [TAG=suffix] tools/gpu_check.sh [tests|smoke|bench|bench-<config>|prof|pmc ...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -18,13 +18,13 @@ for s in "${steps[@]}"; do
   case "$s" in
     tests) timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
-    bench) timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 ;;
+    bench) timeout -k 10 600 python bench.py > gpurun_out/bench${TAG:-}.log 2>&1 ;;
     bench-*) timeout -k 10 900 python bench.py --config "${s#bench-}" --no-cpu-baseline > "gpurun_out/bench_${s#bench-}.log" 2>&1 ;;
-    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-            python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 > gpurun_out/prof.log 2>&1 ;;
-    pmc) timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- \
+    prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof${TAG:-} -o run --output-format csv -- \
+            python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 > gpurun_out/prof${TAG:-}.log 2>&1 ;;
+    pmc) timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch${TAG:-} -o run --output-format csv -- \
             python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > gpurun_out/pmc_fetch.log 2>&1 && \
-         timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- \
+         timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write${TAG:-} -o run --output-format csv -- \
             python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 > gpurun_out/pmc_write.log 2>&1 ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac

@@ -23,7 +23,9 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 }
 
 // MODE bits: 1 = gather from row 0 (no randomness), 2 = fp32 math, 4 = no stores,
-//            8 = no gathers at all (use list value), 16 = bias folded in padded table
+//            8 = no gathers at all (use list value), 16 = bias folded in padded table,
+//            32 = nontemporal stores, 64 = sc1 (agent relaxed atomic) stores,
+//            128 = nontemporal list loads, 256 = only the influence store
 template <int RW, int MODE>
 __global__ __launch_bounds__(256) void k_v0(int64_t nchunks, int64_t N, const int* __restrict__ other,
                                             const float* __restrict__ rating, const int* __restrict__ rowi,
@@ -43,9 +45,15 @@ __global__ __launch_bounds__(256) void k_v0(int64_t nchunks, int64_t N, const in
 #pragma unroll
     for (int r = 0; r < RW; ++r) {
       const int64_t li = base + r * 64 + lane;
-      o_[r] = other[li];
-      y_[r] = rating[li];
-      row_[r] = rowi[li];
+      if (MODE & 128) {
+        o_[r] = __builtin_nontemporal_load(other + li);
+        y_[r] = __builtin_nontemporal_load(rating + li);
+        row_[r] = __builtin_nontemporal_load(rowi + li);
+      } else {
+        o_[r] = other[li];
+        y_[r] = rating[li];
+        row_[r] = rowi[li];
+      }
     }
 #pragma unroll
     for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
@@ -106,9 +114,15 @@ __global__ __launch_bounds__(256) void k_v0(int64_t nchunks, int64_t N, const in
       const int64_t li = base + r * 64 + lane;
       if (MODE & 4) {
         asm volatile("" ::"v"(v), "v"(row_[r]));
+      } else if (MODE & 32) {
+        __builtin_nontemporal_store(v, infl + li);
+        if (!(MODE & 256)) __builtin_nontemporal_store((long long)row_[r], rel + li);
+      } else if (MODE & 64) {
+        __hip_atomic_store(infl + li, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!(MODE & 256)) __hip_atomic_store(rel + li, (long long)row_[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         infl[li] = v;
-        rel[li] = row_[r];
+        if (!(MODE & 256)) rel[li] = row_[r];
       }
     }
   }
@@ -233,20 +247,22 @@ int main() {
                                                d_Tp, d_rec, d_inf, d_rel); }, 20);                                 \
     printf("%-34s grid %6d  %8.1f us  %6.2f TB/s (28 B/row)\n", name, (int)(grid), ms * 1e3, bytes / (ms * 1e-3) / 1e12); \
   }
-  for (int grid : {2048, 4096, 8192, 16384}) {
-    RUN("v0 RW4", (k_v0<4, 0>), 4, grid);
-  }
-  RUN("v0 RW2", (k_v0<2, 0>), 2, 8192);
+  RUN("v0 RW4", (k_v0<4, 0>), 4, 8192);
   RUN("v0 RW8", (k_v0<8, 0>), 8, 8192);
-  RUN("v0 RW4 gather row0", (k_v0<4, 1>), 4, 8192);
-  RUN("v0 RW4 fp32 math", (k_v0<4, 2>), 4, 8192);
   RUN("v0 RW4 no stores", (k_v0<4, 4>), 4, 8192);
-  RUN("v0 RW4 no gathers", (k_v0<4, 8>), 4, 8192);
-  RUN("v0 RW4 bias folded", (k_v0<4, 16>), 4, 8192);
-  RUN("v0 RW4 no gathers no stores", (k_v0<4, 12>), 4, 8192);
-  RUN("quad", (k_quad<0>), 4, 8192);
-  RUN("quad bias folded", (k_quad<16>), 4, 8192);
-  RUN("quad row0", (k_quad<1>), 4, 8192);
-  RUN("quad no stores", (k_quad<4>), 4, 8192);
+  RUN("v0 RW4 nt stores", (k_v0<4, 32>), 4, 8192);
+  RUN("v0 RW4 sc1 stores", (k_v0<4, 64>), 4, 8192);
+  RUN("v0 RW4 nt loads", (k_v0<4, 128>), 4, 8192);
+  RUN("v0 RW4 nt loads+stores", (k_v0<4, 160>), 4, 8192);
+  RUN("v0 RW4 infl only", (k_v0<4, 256>), 4, 8192);
+  RUN("v0 RW8 nt stores", (k_v0<8, 32>), 8, 8192);
+  RUN("v0 RW8 nt loads+stores", (k_v0<8, 160>), 8, 8192);
+  RUN("v0 RW8 sc1 stores", (k_v0<8, 64>), 8, 8192);
+  RUN("v0 RW8 no stores", (k_v0<8, 4>), 8, 8192);
+  RUN("v0 RW8 gather row0", (k_v0<8, 1>), 8, 8192);
+  RUN("v0 RW6", (k_v0<6, 0>), 6, 8192);
+  RUN("v0 RW6 nt stores", (k_v0<6, 32>), 6, 8192);
+  RUN("v0 RW8 grid 4096", (k_v0<8, 0>), 8, 4096);
+  RUN("v0 RW8 grid 16384", (k_v0<8, 0>), 8, 16384);
   return 0;
 }
