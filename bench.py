@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="ml1m-mf", choices=sorted(CONFIGS))
     ap.add_argument("--topk", type=int, default=1)
+    ap.add_argument("--batch-rows", type=int, default=1 << 29,
+                    help="max related ratings per fia_query_batch call (output buffers are reused)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
@@ -142,21 +144,39 @@ def main():
     index_s = time.time() - t0
     qu = torch.from_numpy(qu_np).to(dev)
     qi = torch.from_numpy(qi_np).to(dev)
-    offsets, total = ctx.count_related(qu, qi)
-    n_q = np.diff(offsets.cpu().numpy())
+    offsets_all, _ = ctx.count_related(qu, qi)
+    n_q = np.diff(offsets_all.cpu().numpy())
+    total = int(n_q.sum())
     D = ctx.num_params()
     K = args.topk
-    rel = torch.empty(total, dtype=torch.int64, device=dev)
-    infl = torch.empty(total, dtype=torch.float64, device=dev)
-    xbuf = torch.empty(Q * D, dtype=torch.float64, device=dev)
+    # query batches of <= --batch-rows related ratings (output buffers reused batch to batch;
+    # ml-1m-ex / yelp-ex fit in one batch)
+    cum = np.concatenate([[0], np.cumsum(n_q)])
+    bounds = [0]
+    while bounds[-1] < Q:
+        b0 = bounds[-1]
+        b1 = int(np.searchsorted(cum, cum[b0] + args.batch_rows, side="right")) - 1
+        bounds.append(min(Q, max(b1, b0 + 1)))
+    batches = []
+    for b0, b1 in zip(bounds[:-1], bounds[1:]):
+        qb_u, qb_i = qu[b0:b1], qi[b0:b1]
+        off_b, tot_b = ctx.count_related(qb_u, qb_i)
+        batches.append((b0, b1, qb_u, qb_i, off_b, tot_b))
+    max_rows = max(b[5] for b in batches)
+    max_q = max(b[1] - b[0] for b in batches)
+    rel = torch.empty(max_rows, dtype=torch.int64, device=dev)
+    infl = torch.empty(max_rows, dtype=torch.float64, device=dev)
+    xbuf = torch.empty(max_q * D, dtype=torch.float64, device=dev)
     tp = torch.empty(Q * K, dtype=torch.int64, device=dev)
     tix = torch.empty(Q * K, dtype=torch.int64, device=dev)
     tv = torch.empty(Q * K, dtype=torch.float64, device=dev)
 
     def step():
         ctx.prepare()
-        ctx.count_related(qu, qi, offsets, want_total=False)
-        ctx.query_batch(qu, qi, offsets, total, rel, infl, xbuf, K, tp, tix, tv)
+        for b0, b1, qb_u, qb_i, off_b, tot_b in batches:
+            ctx.count_related(qb_u, qb_i, off_b, want_total=False)
+            ctx.query_batch(qb_u, qb_i, off_b, tot_b, rel, infl, xbuf, K, tp[b0 * K:b1 * K],
+                            tix[b0 * K:b1 * K], tv[b0 * K:b1 * K])
         if world > 1:
             gather_topk(tix.view(Q, K), tv.view(Q, K))
 
@@ -184,8 +204,8 @@ def main():
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * Q * args.steps / elapsed
-    score_ms = phases["score"][0] / max(phases["score"][1], 1)
-    bytes_launch = float(bytes_per_query(cfg["model"], k, n_q).sum())
+    score_ms = phases["score"][0] / max(phases["score"][1], 1)          # per launch
+    bytes_launch = float(bytes_per_query(cfg["model"], k, n_q).sum()) / len(batches)   # mean per launch
     achieved = bytes_launch / (score_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -206,6 +226,7 @@ def main():
                 "real held-out test pairs; synthetic parameters",
         "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_gpu": Q,
                    "n_train": int(tu.size), "related_ratings_per_gpu_step": int(total), "topk": K,
+                   "query_batches": len(batches),
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

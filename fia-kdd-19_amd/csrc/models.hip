@@ -15,6 +15,7 @@
 //   x = H_t^{-1} v by an exact fp64 LDL^T in LDS (replaces fmin_ncg, mf:419-433).
 //   influence_j = x . (2 e_j g_j + wd*M*theta_t) / n (mf:237-246).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -381,6 +382,132 @@ __device__ void ldlt_solve(double* H, double* v, double* d, double* w, int lo, i
   }
 }
 
+// Packed column-major lower storage: column c (rows c..N-1) starts at cs(c).
+template <int N>
+__device__ __forceinline__ int cs(int c) { return c * N - (c * (c - 1)) / 2; }
+
+// Two independent N x N systems (the user and the item block of one query; the path for
+// blocks too large for solve_blocks_regs), each a packed column-major lower block
+// H + b*PN with right-hand side v + b*N, solved in place by a right-looking LDL^T in which
+// every lane owns whole columns: step j, lane c > j does A[r][c] -= A[r][j] * (A[c][j] /
+// A[j][j]) down its own column (rows r >= c).  The blocks go in turn, lane c owning
+// columns c, c + 64.
+template <int N>
+__device__ void ldlt_cols(double* __restrict__ Hb, double* __restrict__ vb) {
+  constexpr int PN = N * (N + 1) / 2;
+  constexpr int CSTEP = kSolveThreads;
+  const int lane = threadIdx.x;
+#pragma unroll 1
+  for (int b = 0; b < 2; ++b) {
+    const int cl = lane;
+    double* H = Hb + b * PN;
+    double* v = vb + b * N;
+    for (int j = 0; j < N; ++j) {
+      __syncthreads();
+      const double* Hj = H + cs<N>(j) - j;     // Hj[r] = A[r][j]
+      const double dj = Hj[j];
+      for (int c = cl; c < N; c += CSTEP) {
+        if (c > j) {
+          const double f = Hj[c] / dj;
+          double* Hc = H + cs<N>(c) - c;       // Hc[r] = A[r][c]
+          for (int r = c; r < N; ++r) Hc[r] = fma(-Hj[r], f, Hc[r]);
+        }
+      }
+    }
+    __syncthreads();
+    for (int c = cl; c < N; c += CSTEP) {      // L[r][c] = A[r][c] / d_c
+      double* Hc = H + cs<N>(c) - c;
+      const double inv = 1.0 / Hc[c];
+      for (int r = c + 1; r < N; ++r) Hc[r] *= inv;
+    }
+    for (int j = 0; j < N; ++j) {              // L y = v
+      __syncthreads();
+      const double yj = v[j];
+      const double* Lj = H + cs<N>(j) - j;
+      for (int r = cl; r < N; r += CSTEP)
+        if (r > j) v[r] = fma(-Lj[r], yj, v[r]);
+    }
+    __syncthreads();
+    for (int r = cl; r < N; r += CSTEP) v[r] /= H[cs<N>(r)];
+    for (int j = N - 1; j >= 0; --j) {         // L^T x = D^-1 y
+      __syncthreads();
+      const double xj = v[j];
+      for (int c = cl; c < N; c += CSTEP)
+        if (c < j) v[c] = fma(-(H + cs<N>(c) - c)[j], xj, v[c]);
+    }
+    __syncthreads();
+  }
+}
+
+// Register-resident solve of the two blocks of a query (N = Ds <= 64): lane c holds column c
+// of the symmetric block (all N rows), fully unrolled right-looking LDL^T whose pivot
+// column is broadcast lane j -> all (v_readlane; with 2N <= 64 both blocks run at once in
+// the two 32-lane halves and the broadcast is a 32-wide shuffle).  After step j lane c > j
+// keeps L[c][j] in col[j] (forward solve) and its own column below the diagonal holds
+// d_c L[r][c] (backward solve).  g: right-hand sides [2N] (LDS), v: solutions [2N] (LDS).
+template <int N>
+__device__ __forceinline__ double bcast_col(double x, int j) {
+  if constexpr (2 * N <= 64) return __shfl(x, j, 32);
+  else return readlane_d(x, j);
+}
+
+template <class M>
+__device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* __restrict__ Gi, double s2n,
+                                  double wd, double damping, const double* __restrict__ g, double* __restrict__ v,
+                                  double* __restrict__ Hs) {
+  constexpr int N = M::Ds, GS = N * (N + 1) / 2;
+  static_assert(N <= 64, "one column per lane");
+  constexpr bool PAR = 2 * N <= 64;
+  const int lane = threadIdx.x;
+  // both cached blocks into LDS with coalesced loads; the per-lane column reads below are
+  // strided (A[r][c] for r < c sits in row c of the packed lower layout)
+  for (int t = lane; t < GS; t += kSolveThreads) {
+    Hs[t] = Gu[t];
+    Hs[GS + t] = Gi[t];
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int b0 = 0; b0 < (PAR ? 1 : 2); ++b0) {
+    const int b = PAR ? lane >> 5 : b0;
+    const int c = PAR ? lane & 31 : lane;
+    const bool live = c < N;
+    const double* __restrict__ Gb = Hs + b * GS;
+    double col[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const int hi = r > c ? r : c, lo = r > c ? c : r;
+      col[r] = live ? s2n * Gb[tri(hi, lo)] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+      if (r == c) col[r] += (M::decayed(r) ? wd : 0.0) + damping;
+    double y = live ? g[b * N + c] : 0.0;
+    double dinv_own = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double ij = 1.0 / bcast_col<N>(col[j], j);
+      if (c == j) dinv_own = ij;
+      const double f = c > j ? col[j] * ij : 0.0;
+#pragma unroll
+      for (int r = j + 1; r < N; ++r) col[r] = fma(-bcast_col<N>(col[r], j), f, col[r]);
+      if (c > j) col[j] = f;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {             // L y = g
+      const double yi = bcast_col<N>(y, i);
+      if (c > i) y = fma(-col[i], yi, y);
+    }
+    y *= dinv_own;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {        // L^T x = D^-1 y
+      const double xj = bcast_col<N>(y, j);
+      if (c < j) y = fma(-col[j] * dinv_own, xj, y);
+    }
+    if (live) v[b * N + c] = y;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ double wave_sum(double x) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
@@ -402,15 +529,28 @@ struct QueryArgs {
   PairTable pairs;
 };
 
-// One wave per query (general D; the path for NCF, MF k >= 32 and for queries whose
-// test pair is itself a train row).  qlist (nullable): {count, q_0, q_1, ...}.
-template <class M>
+// One wave per query.  COLS: the two blocks of a query whose test pair is not a train row
+// are solved by ldlt_cols (the path for NCF and MF k >= 32); queries whose pair IS a train
+// row (coupled blocks) are appended to `coupled` {count, q...} for the full-D launch.
+// !COLS: the full D x D packed LDL^T (coupled queries, or every query of qlist).
+// qlist (nullable): {count, q_0, q_1, ...}.
+template <class M, bool COLS>
 __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist) {
+                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist,
+                                                         int32_t* __restrict__ coupled_out) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
-  __shared__ double H[D * (D + 1) / 2];
+  __shared__ double H[COLS ? 2 * GS : D * (D + 1) / 2];
   __shared__ double v[D], g[D], th[D], dd[D], ww[D];
   __shared__ double sh[4 * K + 8];
+  // NCF weights staged once per block (fp64), read by every query the block solves
+  __shared__ NCFWeights<M::ncf ? K : 2> w;
+  __shared__ double sW1[M::ncf ? 2 * K * K : 1];
+  __shared__ double sb1[M::ncf ? K : 1];
+  if constexpr (M::ncf) {
+    load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
+    for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
+    for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
+  }
   const int64_t nwork = qlist ? (int64_t)qlist[0] : Q;
   for (int64_t wk = blockIdx.x; wk < nwork; wk += gridDim.x) {
   __syncthreads();
@@ -457,11 +597,6 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
     const float* Qm = A.t[1];
     const float* Pg = A.t[2];
     const float* Qg = A.t[3];
-    const float* W1 = A.t[4];
-    const float* b1 = A.t[5];
-    const float* W2 = A.t[6];
-    const float* b2 = A.t[7];
-    const float* W3 = A.t[8];
     double* z1 = sh;            // K
     double* d2 = sh + K;        // K/2
     double* d1 = sh + 2 * K;    // K
@@ -470,36 +605,36 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
       th[K + a] = Pg[(int64_t)u * K + a];
       th[Ds + a] = Qm[(int64_t)i * K + a];
       th[Ds + K + a] = Qg[(int64_t)i * K + a];
-      z1[a] = A.l1[0][(int64_t)u * K + a] + A.l1[1][(int64_t)i * K + a] + (double)b1[a];
+      z1[a] = A.l1[0][(int64_t)u * K + a] + A.l1[1][(int64_t)i * K + a] + sb1[a];
     }
     __syncthreads();
     double mlp_part = 0.0;
     for (int dd2 = lane; dd2 < H2; dd2 += kSolveThreads) {
-      double z2 = b2[dd2];
-      for (int c = 0; c < K; ++c) z2 = fma((double)W2[c * H2 + dd2], z1[c] > 0.0 ? z1[c] : 0.0, z2);
+      double z2 = w.b2[dd2];
+      for (int c = 0; c < K; ++c) z2 = fma(w.W2[c * H2 + dd2], z1[c] > 0.0 ? z1[c] : 0.0, z2);
       const bool on = z2 > 0.0;
-      d2[dd2] = on ? (double)W3[dd2] : 0.0;
-      mlp_part += on ? (double)W3[dd2] * z2 : 0.0;
+      d2[dd2] = on ? w.W3[dd2] : 0.0;
+      mlp_part += on ? w.W3[dd2] * z2 : 0.0;
     }
     double gmf_part = 0.0;
-    for (int a = lane; a < K; a += kSolveThreads) gmf_part += (double)W3[H2 + a] * th[K + a] * th[Ds + K + a];
+    for (int a = lane; a < K; a += kSolveThreads) gmf_part += w.W3[H2 + a] * th[K + a] * th[Ds + K + a];
     rhat_ui = wave_sum(mlp_part + gmf_part) + (double)A.t[9][0];
     __syncthreads();
     for (int c = lane; c < K; c += kSolveThreads) {
       double t = 0.0;
-      for (int dd2 = 0; dd2 < H2; ++dd2) t = fma((double)W2[c * H2 + dd2], d2[dd2], t);
+      for (int dd2 = 0; dd2 < H2; ++dd2) t = fma(w.W2[c * H2 + dd2], d2[dd2], t);
       d1[c] = z1[c] > 0.0 ? t : 0.0;
     }
     __syncthreads();
     for (int a = lane; a < 2 * K; a += kSolveThreads) {
       // rows a < K: W1[:k] (Pm part, user block); rows a >= K: W1[k:] (Qm part, item block)
       double s = 0.0;
-      for (int c = 0; c < K; ++c) s = fma((double)W1[a * K + c], d1[c], s);
+      for (int c = 0; c < K; ++c) s = fma(sW1[a * K + c], d1[c], s);
       if (a < K) g[a] = s; else g[Ds + (a - K)] = s;
     }
     for (int a = lane; a < K; a += kSolveThreads) {
-      g[K + a] = (double)W3[H2 + a] * th[Ds + K + a];        // d r/d Pg_u = W3g * Qg_i
-      g[Ds + K + a] = (double)W3[H2 + a] * th[K + a];        // d r/d Qg_i = W3g * Pg_u
+      g[K + a] = w.W3[H2 + a] * th[Ds + K + a];        // d r/d Pg_u = W3g * Qg_i
+      g[Ds + K + a] = w.W3[H2 + a] * th[K + a];        // d r/d Qg_i = W3g * Pg_u
     }
   }
   __syncthreads();
@@ -510,43 +645,70 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
   const bool coupled = cdup > 0.0;
   const double esum = cdup * rhat_ui - rsum;
 
-  // ---- assemble H (packed lower, D x D) ----
+  // ---- assemble H and solve ----
   const double* Gu = A.gram[0] + (int64_t)u * ((GS + 1) & ~1);
   const double* Gi = A.gram[1] + (int64_t)i * ((GS + 1) & ~1);
-  for (int t = lane; t < D * (D + 1) / 2; t += kSolveThreads) {
-    int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-    while (tri(r + 1, 0) <= t) ++r;
-    while (tri(r, 0) > t) --r;
-    const int c = t - tri(r, 0);
-    double h = 0.0;
-    if (r < Ds) {
-      h = s2n * (Gu[tri(r, c)] + cdup * g[r] * g[c]);
-    } else if (c >= Ds) {
-      const int rr = r - Ds, cc = c - Ds;
-      h = s2n * (Gi[tri(rr, cc)] + cdup * g[r] * g[c]);
-    } else if (coupled) {
-      // cross block: item row rr, user col c: 2 (c g_i g_u^T + esum * d2r/dtheta_i dtheta_u)
-      const int rr = r - Ds;
-      h = s2n * 2.0 * cdup * g[r] * g[c];
-      if constexpr (!M::ncf) {
-        if (rr == c && c < K) h += s2n * 2.0 * esum;                     // d2 r / dp_u dq_i = I
-      } else {
-        if (rr == c && c >= K) h += s2n * 2.0 * esum * (double)A.t[8][K / 2 + (c - K)];   // diag(W3g)
+  if constexpr (COLS) {
+    if (coupled) {
+      if (lane == 0) {
+        const int slot = atomicAdd(coupled_out, 1);
+        coupled_out[1 + slot] = (int32_t)q;
       }
+      continue;
     }
-    if (r == c) h += (M::decayed(r < Ds ? r : r - Ds) ? A.wd : 0.0) + A.damping;
-    H[t] = h;
-  }
-  for (int a = lane; a < D; a += kSolveThreads) v[a] = g[a];
-  __syncthreads();
-
-  if (coupled) {
-    ldlt_solve<D>(H, v, dd, ww, 0, D);
+    if constexpr (M::Ds <= 64) {
+      solve_blocks_regs<M>(Gu, Gi, s2n, A.wd, A.damping, g, v, H);
+    } else {
+      // block b: H_b = (2/n) Gram_b + wd on decayed coordinates + damping, column-major
+      for (int t = lane; t < 2 * GS; t += kSolveThreads) {
+        const int b = t >= GS, tt = t - b * GS;
+        int r = (int)((sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
+        while (tri(r + 1, 0) <= tt) ++r;
+        while (tri(r, 0) > tt) --r;
+        const int c = tt - tri(r, 0);
+        double h = s2n * (b ? Gi : Gu)[tt];
+        if (r == c) h += (M::decayed(r) ? A.wd : 0.0) + A.damping;
+        H[b * GS + cs<Ds>(c) + (r - c)] = h;
+      }
+      for (int a = lane; a < D; a += kSolveThreads) v[a] = g[a];
+      ldlt_cols<Ds>(H, v);
+    }
   } else {
-    ldlt_solve<D>(H, v, dd, ww, 0, Ds);
-    ldlt_solve<D>(H, v, dd, ww, Ds, D);
+    for (int t = lane; t < D * (D + 1) / 2; t += kSolveThreads) {
+      int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      while (tri(r + 1, 0) <= t) ++r;
+      while (tri(r, 0) > t) --r;
+      const int c = t - tri(r, 0);
+      double h = 0.0;
+      if (r < Ds) {
+        h = s2n * (Gu[tri(r, c)] + cdup * g[r] * g[c]);
+      } else if (c >= Ds) {
+        const int rr = r - Ds, cc = c - Ds;
+        h = s2n * (Gi[tri(rr, cc)] + cdup * g[r] * g[c]);
+      } else if (coupled) {
+        // cross block: item row rr, user col c: 2 (c g_i g_u^T + esum * d2r/dtheta_i dtheta_u)
+        const int rr = r - Ds;
+        h = s2n * 2.0 * cdup * g[r] * g[c];
+        if constexpr (!M::ncf) {
+          if (rr == c && c < K) h += s2n * 2.0 * esum;                     // d2 r / dp_u dq_i = I
+        } else {
+          if (rr == c && c >= K) h += s2n * 2.0 * esum * (double)A.t[8][K / 2 + (c - K)];   // diag(W3g)
+        }
+      }
+      if (r == c) h += (M::decayed(r < Ds ? r : r - Ds) ? A.wd : 0.0) + A.damping;
+      H[t] = h;
+    }
+    for (int a = lane; a < D; a += kSolveThreads) v[a] = g[a];
+    __syncthreads();
+
+    if (coupled) {
+      ldlt_solve<D>(H, v, dd, ww, 0, D);
+    } else {
+      ldlt_solve<D>(H, v, dd, ww, 0, Ds);
+      ldlt_solve<D>(H, v, dd, ww, Ds, D);
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   // ---- outputs ----
   if (x_out)
@@ -586,20 +748,17 @@ __global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q,
     }
   } else {
     constexpr int H2 = K / 2;
-    const float* W1 = A.t[4];
-    const float* b1 = A.t[5];
-    const float* W3 = A.t[8];
     for (int c = lane; c < K; c += kSolveThreads) {
-      S0[c] = A.l1[0][(int64_t)u * K + c] + (double)b1[c];
-      S1[c] = A.l1[1][(int64_t)i * K + c] + (double)b1[c];
+      S0[c] = A.l1[0][(int64_t)u * K + c] + sb1[c];
+      S1[c] = A.l1[1][(int64_t)i * K + c] + sb1[c];
       double y0 = 0.0, y1 = 0.0;
       for (int a = 0; a < K; ++a) {
-        y0 = fma(v[a], (double)W1[a * K + c], y0);
-        y1 = fma(v[Ds + a], (double)W1[(K + a) * K + c], y1);
+        y0 = fma(v[a], sW1[a * K + c], y0);
+        y1 = fma(v[Ds + a], sW1[(K + a) * K + c], y1);
       }
       S0[K + c] = y0;
       S1[K + c] = y1;
-      const double w3g = (double)W3[H2 + c];
+      const double w3g = w.W3[H2 + c];
       S0[2 * K + c] = w3g * v[K + c];
       S1[2 * K + c] = w3g * v[Ds + K + c];
       S0[3 * K + c] = w3g * th[K + c];
@@ -815,6 +974,123 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(int64_t n_items, const int3
     if (grp == 0 && 16 * t + col < K) out[tri(K, 16 * t + col)] = s;
   }
   if (lane == 0) out[tri(K, K)] = (double)len;
+}
+
+// ------------------------------------------------------------------------------------
+// NCF Gram on the f64 matrix cores.  A wave takes one work item (<= kGramChunk ratings
+// of one entity's list) in rounds of 64 ratings: lane l runs rating l's MLP forward and
+// backward (TF ReluGrad masks) and writes its g row -- [W1_side . d1 (k) ;
+// W3g * gmf_other (k)] -- to the wave's LDS tile; then C += G^T G by
+// v_mfma_f64_16x16x4_f64 over the tile's row-quads (lane l reads G[4s + l/16][16t + l%16],
+// both the A and the B operand; same map as k_gram_mf_mfma).
+// ------------------------------------------------------------------------------------
+template <class M>
+struct NCFGramCfg {
+  static constexpr int WAVES = M::K <= 16 ? 4 : 2;          // LDS: 64 rows x (2k+1) doubles per wave
+  static constexpr int LDG = 2 * M::K + 1;
+};
+
+template <class M>
+__global__ __launch_bounds__(256) void k_gram_ncf_mfma(
+    int side, int64_t n_items, const int32_t* __restrict__ items, const int64_t* __restrict__ ptr,
+    const int32_t* __restrict__ other, const float* __restrict__ gmf_other, const double* __restrict__ l1_self,
+    const double* __restrict__ l1_other, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ W3,
+    double* __restrict__ gram, double* __restrict__ part) {
+  constexpr int K = M::K, H = K / 2, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  constexpr int NT = Ds / 16, NP = NT * (NT + 1) / 2;
+  constexpr int WAVES = NCFGramCfg<M>::WAVES, LDG = NCFGramCfg<M>::LDG;
+  static_assert(M::ncf && Ds % 16 == 0 && K <= 64, "NCF Gram tiling");
+  __shared__ NCFWeights<K> w;
+  __shared__ double W1s[K * K];     // this side's half of W1, [a][c]
+  __shared__ double w3g[K];
+  __shared__ double gl[WAVES][64 * LDG];
+  for (int t = threadIdx.x; t < K * K; t += blockDim.x) W1s[t] = (double)W1[side * K * K + t];
+  for (int t = threadIdx.x; t < K; t += blockDim.x) w3g[t] = (double)W3[H + t];
+  load_ncf_weights<K>(w, W2, b2, W3);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  double* __restrict__ G = gl[wave];
+  for (int64_t it = (int64_t)blockIdx.x * WAVES + wave; it < n_items; it += (int64_t)gridDim.x * WAVES) {
+    const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], slot = items[4 * it + 3];
+    const int32_t* ids = other + ptr[e] + start;
+    // the entity's own layer-1 half + b1, spread over lanes
+    const double selfv = lane < K ? l1_self[(int64_t)e * K + lane] + (double)b1[lane] : 0.0;
+    d4_t acc[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
+    for (int t0 = 0; t0 < len; t0 += 64) {
+      const bool valid = t0 + lane < len;
+      const int32_t o = ids[valid ? t0 + lane : 0];
+      const double* L1o = l1_other + (int64_t)o * K;
+      const float* Go = gmf_other + (int64_t)o * K;
+      double z2[H];
+#pragma unroll
+      for (int d = 0; d < H; ++d) z2[d] = w.b2[d];
+      uint64_t mask = 0;
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const double z = readlane_d(selfv, c) + L1o[c];
+        mask |= (uint64_t)(z > 0.0) << c;
+        const double h = z > 0.0 ? z : 0.0;
+#pragma unroll
+        for (int d = 0; d < H; ++d) z2[d] = fma(w.W2[c * H + d], h, z2[d]);
+      }
+#pragma unroll
+      for (int d = 0; d < H; ++d) z2[d] = z2[d] > 0.0 ? w.W3[d] : 0.0;   // d2
+      double d1[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        double t = 0.0;
+#pragma unroll
+        for (int d = 0; d < H; ++d) t = fma(w.W2[c * H + d], z2[d], t);
+        d1[c] = (mask >> c) & 1 ? t : 0.0;
+      }
+      double* gr = G + lane * LDG;
+#pragma unroll
+      for (int a = 0; a < K; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < K; ++c) s = fma(W1s[a * K + c], d1[c], s);
+        gr[a] = valid ? s : 0.0;
+        gr[K + a] = valid ? w3g[a] * (double)Go[a] : 0.0;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int nquad = (len - t0 + 3) >> 2;     // row-quads holding real ratings
+#pragma unroll 4
+      for (int sq = 0; sq < 16; ++sq) {
+        if (sq >= nquad) break;
+        double av[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) av[t] = G[(4 * sq + grp) * LDG + 16 * t + col];
+        int p = 0;
+#pragma unroll
+        for (int ta = 0; ta < NT; ++ta)
+#pragma unroll
+          for (int tb = ta; tb < NT; ++tb, ++p)
+            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ta], av[tb], acc[p], 0, 0, 0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();    // the tile is consumed before the next round rewrites it
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    double* out = slot < 0 ? gram + (int64_t)e * GSP : part + (int64_t)slot * GSP;
+    int p = 0;
+#pragma unroll
+    for (int ta = 0; ta < NT; ++ta)
+#pragma unroll
+      for (int tb = ta; tb < NT; ++tb, ++p)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int ci = 16 * ta + grp + 4 * rr;    // C row -> Gram column index (tile ta)
+          const int rj = 16 * tb + col;             // C col -> Gram row index (tile tb)
+          if (rj >= ci) out[tri(rj, ci)] = acc[p][rr];
+        }
+  }
 }
 
 // Sum the partial Grams of split lists in slot order (deterministic).
@@ -1360,29 +1636,31 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   }
   for (int sd = 0; sd < 2; ++sd) {
     if (n_ent[sd] == 0) continue;
-    const float* emb_other;
-    if constexpr (M::ncf) emb_other = c->p.t[sd == 0 ? 3 : 2];   // gmf table of the other side
-    else emb_other = c->p.t[sd == 0 ? 1 : 0];
-    if constexpr (!M::ncf) {
-      constexpr int GSP = (GS + 1) & ~1;
-      const Index& X = c->idx;
-      if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
-      hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)X.n_gitems[sd]), dim3(64), 0, s, X.n_gitems[sd],
-                         X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
-                         emb_other, c->gram[sd].as<double>(), c->gpart[sd].as<double>());
-      FIA_HIP_TRY(hipGetLastError());
-      if (X.n_gcomb[sd] > 0) {
-        hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)X.n_gcomb[sd]), dim3(64), 0, s, X.n_gcomb[sd],
-                           X.gcomb[sd].as<int32_t>(), GS, GSP, c->gpart[sd].as<double>(), c->gram[sd].as<double>());
-        FIA_HIP_TRY(hipGetLastError());
+    constexpr int GSP = (GS + 1) & ~1;
+    const Index& X = c->idx;
+    if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
+    if (X.n_gitems[sd] > 0) {
+      if constexpr (M::ncf) {
+        constexpr int WAVES = NCFGramCfg<M>::WAVES;
+        int64_t grid = (X.n_gitems[sd] + WAVES - 1) / WAVES;
+        if (grid > 16384) grid = 16384;
+        hipLaunchKernelGGL(k_gram_ncf_mfma<M>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, sd, X.n_gitems[sd],
+                           X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
+                           c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4],
+                           c->p.t[5], c->p.t[6], c->p.t[7], c->p.t[8], c->gram[sd].as<double>(),
+                           c->gpart[sd].as<double>());
+      } else {
+        hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)X.n_gitems[sd]), dim3(64), 0, s, X.n_gitems[sd],
+                           X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
+                           c->p.t[sd == 0 ? 1 : 0], c->gram[sd].as<double>(), c->gpart[sd].as<double>());
       }
-      continue;
+      FIA_HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_gram<M>, dim3((unsigned)n_ent[sd]), dim3(kPrepThreads), 0, s, sd, n_ent[sd],
-                       c->idx.side[sd].ptr.as<int64_t>(), c->idx.side[sd].other.as<int32_t>(), emb_other,
-                       c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4], c->p.t[5], c->p.t[6],
-                       c->p.t[7], c->p.t[8], c->gram[sd].as<double>());
-    FIA_HIP_TRY(hipGetLastError());
+    if (X.n_gcomb[sd] > 0) {
+      hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)X.n_gcomb[sd]), dim3(64), 0, s, X.n_gcomb[sd],
+                         X.gcomb[sd].as<int32_t>(), GS, GSP, c->gpart[sd].as<double>(), c->gram[sd].as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
   }
   return hipSuccess;
 }
@@ -1408,18 +1686,23 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
-  if constexpr (use_tps<M>()) {
-    FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
-    FIA_HIP_TRY(hipMemsetAsync(c->coupled.ptr, 0, sizeof(int32_t), s));
-    hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
-                       c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+  // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks; the
+  // queries whose test pair is a train row are listed in `coupled` and solved full-D
+  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
+  FIA_HIP_TRY(hipMemsetAsync(c->coupled.ptr, 0, sizeof(int32_t), s));
+  if (Q > 0) {
+    if constexpr (use_tps<M>()) {
+      hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
+                         c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+    } else {
+      const int64_t g1 = Q < 2048 ? Q : 2048;     // persistent: weights staged once per block
+      hipLaunchKernelGGL((k_solve<M, true>), dim3((unsigned)g1), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
+                         x_out, (const int32_t*)nullptr, c->coupled.as<int32_t>());
+    }
     FIA_HIP_TRY(hipGetLastError());
     const int64_t g2 = Q < 1024 ? Q : 1024;
-    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
-                       (const int32_t*)c->coupled.as<int32_t>());
-  } else {
-    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)Q), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
-                       (const int32_t*)nullptr);
+    hipLaunchKernelGGL((k_solve<M, false>), dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
+                       x_out, (const int32_t*)c->coupled.as<int32_t>(), (int32_t*)nullptr);
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
