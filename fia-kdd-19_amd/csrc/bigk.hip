@@ -1,0 +1,1117 @@
+// Large-k FIA path: MF k in {128, 256} (side blocks of 129 / 257 coordinates) and
+// NCF k in {64, 128, 256} (side blocks of 128 / 256 / 512) -- BASELINE.json config 5
+// ("512x512 per-query Hessians, FP64 MFMA Cholesky").  Same math as models.hip
+// (mf:164-251, ncf:193-280):
+//
+//   H_t = (2/n) (A_u (+) B_i) + wd*M + damping*I   (+ coupling iff (u,i) is a train row)
+//   x   = H_t^{-1} v,   influence_j = (2 e_j x.g_j + wd x.(M theta)) / n
+//
+// but every structure is sized for blocks that do not fit a wave's registers or a
+// CU's LDS:
+//   * per train row, once per prepare: the residual e_j = r-hat_j - y_j and (NCF) the
+//     masked MLP backward vector d1_j (k_resid_mf / k_ncf_rows, the NCF one as three
+//     f64-MFMA products per 16 ratings);
+//   * per entity: the Gram A_e = sum g g^T in 16x16 tiles (tile-packed lower, fp64),
+//     accumulated on v_mfma_f64_16x16x4_f64 from 16-rating slabs staged in LDS
+//     (k_big_gram; long lists split into slices, partials summed in slot order);
+//   * per (query, side) block -- or per query when the blocks couple -- a blocked
+//     left-looking LDL^T (k_big_solve): each 32-column panel is updated from the
+//     already-factored columns with MFMA (L streamed from a per-workgroup scratch,
+//     D L^T on the fly), factored in LDS, written back.  The right-hand side v rides
+//     along as the matrix's extra last row, so its row of L is D^-1 L^-1 v and only the
+//     backward solve L^T x = y remains;
+//   * scoring over entity chunks shared by every query of the batch with that entity
+//     (k_big_score): the gathered rows / d1_j / e_j are loaded once per chunk and
+//     dotted with up to 8 query vectors.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+
+namespace fia {
+namespace {
+
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
+// C += A B on the f64 matrix cores; lane l supplies A[l&15][l>>4] and B[l>>4][l&15],
+// and holds C[(l>>4) + 4r][l&15] in register r.
+__device__ __forceinline__ d4_t mfma4(double a, double b, d4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ double wsum(double x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+
+// block-wide sum for 256-thread blocks (every thread gets the result)
+__device__ __forceinline__ double bsum256(double x, double* red) {
+  x = wsum(x);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+__device__ __forceinline__ double topk_key(double v) {
+  double a = fabs(v);
+  return (a != a) ? -1.0 : a;
+}
+__device__ __forceinline__ bool better(double a1, int p1, double a2, int p2) {
+  return a1 > a2 || (a1 == a2 && p1 < p2);
+}
+__device__ __forceinline__ void wave_best(double& a, int& p, double& v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double oa = __shfl_xor(a, off);
+    int op = __shfl_xor(p, off);
+    double ov = __shfl_xor(v, off);
+    if (better(oa, op, a, p)) { a = oa; p = op; v = ov; }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// model traits.  A side block has Ds coordinates padded to NPs = 16 T.
+//   MF  side [emb (k), bias, 0 pad]  (mf:43-65)    record [x_emb (k), x_bias, dup_other]
+//   NCF side [mlp emb (k), gmf emb (k)] (ncf:49-64) record [W1_s^T x_mlp (k), W3g*x_gmf (k), dup_other]
+// per-query record: [1/n, c_q, x.v, r-hat(u,i), cq_u, xv_u, cq_i, xv_i, side 0, side 1]
+// per-query work:   [n, cdup, esum, r-hat, coupled, -, -, -, v_u, v_i, theta_u, theta_i]
+// ------------------------------------------------------------------------------------
+template <int K_>
+struct BMF {
+  static constexpr int K = K_, H = 1, Ds = K + 1, NPs = K + 16, T = NPs / 16;
+  static constexpr bool ncf = false;
+  static constexpr int SB = K + 2, R = 8 + 2 * SB, QW = 8 + 4 * NPs;
+  __host__ __device__ static constexpr bool decayed(int a) { return a < K; }
+  // reference theta order [p_u, q_i, b_u, b_i]
+  __device__ static int ref_index(int side, int a) { return a < K ? side * K + a : 2 * K + side; }
+};
+
+template <int K_>
+struct BNCF {
+  static constexpr int K = K_, H = K / 2, Ds = 2 * K, NPs = 2 * K, T = NPs / 16;
+  static constexpr bool ncf = true;
+  static constexpr int SB = 2 * K + 1, R = 8 + 2 * SB, QW = 8 + 4 * NPs;
+  __host__ __device__ static constexpr bool decayed(int) { return true; }
+  // reference theta order [Pm_u, Qm_i, Pg_u, Qg_i]
+  __device__ static int ref_index(int side, int a) { return a < K ? side * K + a : 2 * K + side * K + (a - K); }
+};
+
+// Gram tile storage: tile (tr, tc), tc <= tr, in column-major tile order; inside a tile
+// element (row m, col n) at m + 16 n.
+__host__ __device__ constexpr int tile_off(int T, int tr, int tc) { return tc * T - (tc * (tc - 1)) / 2 + (tr - tc); }
+template <class M>
+constexpr int64_t gram_words() { return (int64_t)M::T * (M::T + 1) / 2 * 256; }
+
+template <class M>
+__device__ __forceinline__ double gram_at(const double* __restrict__ G, int r, int c) {
+  const int hi = r > c ? r : c, lo = r > c ? c : r;
+  return G[tile_off(M::T, hi >> 4, lo >> 4) * 256 + (hi & 15) + 16 * (lo & 15)];
+}
+
+struct BigArgs {
+  const int32_t* qu;
+  const int32_t* qi;
+  int64_t U, I;
+  const int64_t* ptr[2];
+  const int32_t* row[2];
+  const int32_t* other[2];
+  const float* rating[2];
+  const double* gram[2];
+  const double* l1[2];
+  const double* resid;
+  const double* d1;
+  const float* t[10];
+  double wd, damping;
+  PairTable pairs;
+};
+
+// ------------------------------------------------------------------------------------
+// per-position entity of a side's lists: self[p] = e with ptr[e] <= p < ptr[e+1]
+// ------------------------------------------------------------------------------------
+__global__ void k_self(int64_t N, int64_t n_ent, const int64_t* __restrict__ ptr, int32_t* __restrict__ self) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = n_ent;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (ptr[mid] <= p) lo = mid; else hi = mid - 1;
+    }
+    self[p] = (int32_t)lo;
+  }
+}
+
+// MF residual by train row (user-major pass): e_j = p_u.q_i + b_u + b_i + g - y_j (mf:89-116)
+template <int K>
+__global__ void k_resid_mf(int64_t N, const int32_t* __restrict__ self0, const int32_t* __restrict__ other0,
+                           const int32_t* __restrict__ row0, const float* __restrict__ rat0,
+                           const float* __restrict__ P, const float* __restrict__ Qt, const float* __restrict__ bu,
+                           const float* __restrict__ bi, const float* __restrict__ gb, double* __restrict__ resid) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = self0[p], i = other0[p];
+    const float4* a = reinterpret_cast<const float4*>(P + (int64_t)u * K);
+    const float4* b = reinterpret_cast<const float4*>(Qt + (int64_t)i * K);
+    double acc = 0.0;
+#pragma unroll 8
+    for (int c = 0; c < K / 4; ++c) {
+      const float4 x = a[c], y = b[c];
+      acc = fma((double)x.x, (double)y.x, acc);
+      acc = fma((double)x.y, (double)y.y, acc);
+      acc = fma((double)x.z, (double)y.z, acc);
+      acc = fma((double)x.w, (double)y.w, acc);
+    }
+    resid[row0[p]] = acc + (double)bu[u] + (double)bi[i] + (double)gb[0] - (double)rat0[p];
+  }
+}
+
+// NCF layer-1 halves L1[e] = emb_e . W1[row_off : row_off + k]  (fp64)
+template <int K>
+__global__ void k_l1_big(const float* __restrict__ emb, const float* __restrict__ W1, int row_off, int64_t n_ent,
+                         double* __restrict__ out) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_ent * K;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / K;
+    const int c = (int)(t % K);
+    const float* x = emb + e * K;
+    double acc = 0.0;
+    for (int a = 0; a < K; ++a) acc = fma((double)x[a], (double)W1[(int64_t)(row_off + a) * K + c], acc);
+    out[t] = acc;
+  }
+}
+
+// NCF per train row (one wave per 16 user-major list positions), all products on the
+// f64 matrix cores (ncf:102-145, TF ReluGrad masks):
+//   z1 = L1u + L1i + b1,  z2 = relu(z1) W2 + b2,  d2 = 1[z2>0] W3m,
+//   d1 = 1[z1>0] (W2 d2),  r-hat = W3m.relu(z2) + W3g.(Pg_u*Qg_i) + b3
+template <int K>
+__global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __restrict__ self0,
+                                                 const int32_t* __restrict__ other0, const int32_t* __restrict__ row0,
+                                                 const float* __restrict__ rat0, const double* __restrict__ l1u,
+                                                 const double* __restrict__ l1i, const float* __restrict__ b1,
+                                                 const float* __restrict__ W2, const float* __restrict__ b2,
+                                                 const float* __restrict__ W3, const float* __restrict__ b3,
+                                                 const float* __restrict__ Pg, const float* __restrict__ Qg,
+                                                 double* __restrict__ d1s, double* __restrict__ resid) {
+  constexpr int H = K / 2, LZ = K + 4, LD2 = H + 4;
+  __shared__ double Z1[16 * LZ];
+  __shared__ double D2[16 * LD2];
+  const int lane = threadIdx.x;
+  const int ml = lane & 15, kl = lane >> 4;
+  for (int64_t tile = blockIdx.x; tile * 16 < N; tile += gridDim.x) {
+    const int64_t p0 = tile * 16;
+    const int64_t my = p0 + ml;
+    const bool v = my < N;
+    const int32_t u_l = v ? self0[my] : 0, i_l = v ? other0[my] : 0, j_l = v ? row0[my] : 0;
+    const float y_l = v ? rat0[my] : 0.f;
+    __syncthreads();
+    for (int r = 0; r < 16; ++r) {
+      const int32_t u = __shfl(u_l, r), i = __shfl(i_l, r);
+      for (int c = lane; c < K; c += 64)
+        Z1[r * LZ + c] = l1u[(int64_t)u * K + c] + l1i[(int64_t)i * K + c] + (double)b1[c];
+    }
+    __syncthreads();
+    double mlp[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < H / 16; ++t) {
+      d4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+      for (int kk = 0; kk < K; kk += 4) {
+        const double z = Z1[ml * LZ + kk + kl];
+        acc = mfma4(z > 0.0 ? z : 0.0, (double)W2[(kk + kl) * H + 16 * t + ml], acc);
+      }
+      const int d = 16 * t + ml;
+      const double w3m = (double)W3[d], bb = (double)b2[d];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double z2 = acc[r] + bb;
+        const bool on = z2 > 0.0;
+        mlp[r] += on ? w3m * z2 : 0.0;
+        D2[(kl + 4 * r) * LD2 + d] = on ? w3m : 0.0;
+      }
+    }
+    __syncthreads();
+    for (int t = 0; t < K / 16; ++t) {
+      d4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+      for (int kk = 0; kk < H; kk += 4)
+        acc = mfma4(D2[ml * LD2 + kk + kl], (double)W2[(16 * t + ml) * H + kk + kl], acc);
+      const int c = 16 * t + ml;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = kl + 4 * r;
+        const int32_t j = __shfl(j_l, row);
+        if (p0 + row < N) d1s[(int64_t)j * K + c] = Z1[row * LZ + c] > 0.0 ? acc[r] : 0.0;
+      }
+    }
+    // r-hat per row: the MLP part sits in the 16 lanes of group (row & 3), register row >> 2
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double m = mlp[r];
+      m += __shfl_xor(m, 1);
+      m += __shfl_xor(m, 2);
+      m += __shfl_xor(m, 4);
+      m += __shfl_xor(m, 8);
+      mlp[r] = m;
+    }
+    double t0 = __shfl(mlp[0], (ml & 3) * 16), t1 = __shfl(mlp[1], (ml & 3) * 16);
+    double t2 = __shfl(mlp[2], (ml & 3) * 16), t3 = __shfl(mlp[3], (ml & 3) * 16);
+    const int rsel = ml >> 2;
+    const double my_mlp = rsel == 0 ? t0 : rsel == 1 ? t1 : rsel == 2 ? t2 : t3;
+    double my_gmf = 0.0;
+    for (int r = 0; r < 16; ++r) {
+      const int32_t u = __shfl(u_l, r), i = __shfl(i_l, r);
+      double part = 0.0;
+      for (int c = lane; c < K; c += 64)
+        part = fma((double)W3[H + c] * (double)Pg[(int64_t)u * K + c], (double)Qg[(int64_t)i * K + c], part);
+      part = wsum(part);
+      if (ml == r) my_gmf = part;
+    }
+    if (lane < 16 && v) resid[j_l] = my_mlp + my_gmf + (double)b3[0] - (double)y_l;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Entity Gram caches on the f64 matrix cores.  A workgroup (8 waves) takes one slice
+// (<= kBigSlice ratings) of one entity's list and one group of output tiles; per
+// 16 ratings it stages the g rows in LDS (MF: the gathered other-side embedding + 1;
+// NCF: W1_side . d1_j by MFMA + W3g * gmf_other) and every wave adds the rank-16
+// update of its tiles (4 MFMAs per tile).
+// ------------------------------------------------------------------------------------
+constexpr int kGW = 8;              // waves per Gram workgroup
+constexpr int kBigSlice = 2048;     // ratings per Gram work item
+
+template <class M>
+struct GramCfg {
+  static constexpr int NTL = M::T * (M::T + 1) / 2;
+  static constexpr int MAXPER = 18;                                   // accumulator tiles per wave
+  static constexpr int NG = (NTL + kGW * MAXPER - 1) / (kGW * MAXPER);  // tile groups (workgroups per slice)
+  static constexpr int TPG = (NTL + NG - 1) / NG;
+  static constexpr int PER = (TPG + kGW - 1) / kGW;
+  static constexpr int LDG = M::NPs + 16;   // staged g row stride (doubles)
+  static constexpr int LDD = M::K + 4;      // staged d1 row stride
+};
+
+template <class M>
+__global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, const int32_t* __restrict__ items,
+                                                       const int64_t* __restrict__ ptr,
+                                                       const int32_t* __restrict__ other,
+                                                       const int32_t* __restrict__ rowid,
+                                                       const float* __restrict__ emb_other,
+                                                       const double* __restrict__ d1s, const float* __restrict__ W1,
+                                                       const float* __restrict__ W3, double* __restrict__ gram,
+                                                       double* __restrict__ part) {
+  using C = GramCfg<M>;
+  constexpr int K = M::K, T = M::T, LDG = C::LDG, LDD = C::LDD, PER = C::PER;
+  constexpr int64_t GW = gram_words<M>();
+  __shared__ double Gs[16 * LDG];
+  __shared__ double Ds_[M::ncf ? 16 * LDD : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ml = lane & 15, kl = lane >> 4;
+  const int grp = blockIdx.y;
+  const int tend = (grp + 1) * C::TPG < C::NTL ? (grp + 1) * C::TPG : C::NTL;
+  int tr_[PER], tc_[PER];
+  bool on_[PER];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int idx = grp * C::TPG + wave * PER + p;
+    on_[p] = idx < tend;
+    int tr = 0;
+    while ((tr + 1) * (tr + 2) / 2 <= idx) ++tr;
+    tr_[p] = on_[p] ? tr : 0;
+    tc_[p] = on_[p] ? idx - tr * (tr + 1) / 2 : 0;
+  }
+  for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], slot = items[4 * it + 3];
+    const int64_t lb = ptr[e] + start;
+    d4_t acc[PER];
+#pragma unroll
+    for (int p = 0; p < PER; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
+    for (int t0 = 0; t0 < len; t0 += 16) {
+      __syncthreads();
+      {
+        const int r = tid >> 5, pp = tid & 31;   // 16 rows x 32 threads
+        const bool valid = t0 + r < len;
+        const int32_t o = valid ? other[lb + t0 + r] : 0;
+        if constexpr (!M::ncf) {
+          constexpr int PERT = K / 32;            // floats per thread
+          const float* src = emb_other + (int64_t)o * K + pp * PERT;
+#pragma unroll
+          for (int c = 0; c < PERT; c += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(src + c);
+            double* dst = Gs + r * LDG + pp * PERT + c;
+            dst[0] = valid ? (double)x.x : 0.0;
+            dst[1] = valid ? (double)x.y : 0.0;
+            dst[2] = valid ? (double)x.z : 0.0;
+            dst[3] = valid ? (double)x.w : 0.0;
+          }
+          if (pp < 16) Gs[r * LDG + K + pp] = (pp == 0 && valid) ? 1.0 : 0.0;
+        } else {
+          constexpr int PERT = K / 32;
+          const int32_t j = valid ? rowid[lb + t0 + r] : 0;
+          const double* dsrc = d1s + (int64_t)j * K + pp * PERT;
+          const float* gsrc = emb_other + (int64_t)o * K + pp * PERT;
+#pragma unroll
+          for (int c = 0; c < PERT; ++c) {
+            Ds_[r * LDD + pp * PERT + c] = valid ? dsrc[c] : 0.0;
+            Gs[r * LDG + K + pp * PERT + c] = valid ? (double)W3[M::H + pp * PERT + c] * (double)gsrc[c] : 0.0;
+          }
+        }
+      }
+      __syncthreads();
+      if constexpr (M::ncf) {
+        // g_mlp = D1 . W1_side^T  (16 ratings x k), output tiles over the waves
+        for (int at = wave; at < K / 16; at += kGW) {
+          d4_t a4 = {0.0, 0.0, 0.0, 0.0};
+          const float* wrow = W1 + (int64_t)(sd * K + 16 * at + ml) * K;
+#pragma unroll 4
+          for (int kk = 0; kk < K; kk += 4) a4 = mfma4(Ds_[ml * LDD + kk + kl], (double)wrow[kk + kl], a4);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Gs[(kl + 4 * r) * LDG + 16 * at + ml] = a4[r];
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const double* gr = Gs + (4 * s4 + kl) * LDG + ml;
+#pragma unroll
+        for (int p = 0; p < PER; ++p)
+          if (on_[p]) acc[p] = mfma4(gr[16 * tr_[p]], gr[16 * tc_[p]], acc[p]);
+      }
+    }
+    double* out = slot < 0 ? gram + (int64_t)e * GW : part + (int64_t)slot * GW;
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      if (!on_[p]) continue;
+      double* tb = out + (int64_t)tile_off(T, tr_[p], tc_[p]) * 256 + 16 * ml;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tb[kl + 4 * r] = acc[p][r];
+    }
+  }
+}
+
+__global__ void k_big_combine(int64_t n_comb, const int32_t* __restrict__ comb, int64_t GW,
+                              const double* __restrict__ part, double* __restrict__ gram) {
+  for (int64_t w = blockIdx.x; w < n_comb; w += gridDim.x) {
+    const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
+    for (int64_t t = threadIdx.x; t < GW; t += blockDim.x) {
+      double s = 0.0;
+      for (int k = 0; k < ns; ++k) s += part[(int64_t)(first + k) * GW + t];
+      gram[(int64_t)e * GW + t] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Per-query prologue (one 256-thread block per query): n, the pair terms, r-hat(u,i),
+// theta_t and v = d r-hat(u,i) / d theta_t (gnn:155, mf:194,201 / ncf:222,229); append
+// the query's systems to the solve lists.
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(256) void k_big_prologue(BigArgs A, int64_t Q, double* __restrict__ qwork,
+                                                      int32_t* __restrict__ syslist, int32_t* __restrict__ cpllist) {
+  constexpr int K = M::K, NPs = M::NPs;
+  __shared__ double red[4];
+  __shared__ double z1[M::ncf ? K : 1], d2[M::ncf ? M::H : 1], d1[M::ncf ? K : 1];
+  const int tid = threadIdx.x;
+  for (int64_t q = blockIdx.x; q < Q; q += gridDim.x) {
+    const int32_t u = A.qu[q], i = A.qi[q];
+    double* qw = qwork + q * M::QW;
+    const bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
+    const int64_t n = ok ? (A.ptr[0][u + 1] - A.ptr[0][u]) + (A.ptr[1][i + 1] - A.ptr[1][i]) : 0;
+    if (n == 0) {
+      if (tid == 0) qw[0] = 0.0;
+      continue;
+    }
+    double* vu = qw + 8;
+    double* vi = vu + NPs;
+    double* thu = vi + NPs;
+    double* thi = thu + NPs;
+    double rhat;
+    if constexpr (!M::ncf) {
+      const float* P = A.t[0] + (int64_t)u * K;
+      const float* Qt = A.t[1] + (int64_t)i * K;
+      double part = 0.0;
+      for (int a = tid; a < NPs; a += 256) {
+        const double pu = a < K ? (double)P[a] : 0.0, qi = a < K ? (double)Qt[a] : 0.0;
+        part = fma(pu, qi, part);
+        vu[a] = a < K ? qi : (a == K ? 1.0 : 0.0);
+        vi[a] = a < K ? pu : (a == K ? 1.0 : 0.0);
+        thu[a] = a < K ? pu : (a == K ? (double)A.t[2][u] : 0.0);
+        thi[a] = a < K ? qi : (a == K ? (double)A.t[3][i] : 0.0);
+      }
+      rhat = bsum256(part, red) + (double)A.t[2][u] + (double)A.t[3][i] + (double)A.t[4][0];
+    } else {
+      constexpr int H = M::H;
+      const float* W1 = A.t[4];
+      const float* W2 = A.t[6];
+      const float* W3 = A.t[8];
+      __syncthreads();
+      for (int c = tid; c < K; c += 256)
+        z1[c] = A.l1[0][(int64_t)u * K + c] + A.l1[1][(int64_t)i * K + c] + (double)A.t[5][c];
+      __syncthreads();
+      double mlp = 0.0;
+      for (int d = tid; d < H; d += 256) {
+        double z2 = (double)A.t[7][d];
+        for (int c = 0; c < K; ++c) z2 = fma((double)W2[c * H + d], z1[c] > 0.0 ? z1[c] : 0.0, z2);
+        const bool on = z2 > 0.0;
+        mlp += on ? (double)W3[d] * z2 : 0.0;
+        d2[d] = on ? (double)W3[d] : 0.0;
+      }
+      __syncthreads();
+      for (int c = tid; c < K; c += 256) {
+        double t = 0.0;
+        for (int d = 0; d < H; ++d) t = fma((double)W2[c * H + d], d2[d], t);
+        d1[c] = z1[c] > 0.0 ? t : 0.0;
+      }
+      __syncthreads();
+      double gmf = 0.0;
+      for (int a = tid; a < K; a += 256) {
+        double su = 0.0, si = 0.0;
+        for (int c = 0; c < K; ++c) {
+          su = fma((double)W1[(int64_t)a * K + c], d1[c], su);
+          si = fma((double)W1[(int64_t)(K + a) * K + c], d1[c], si);
+        }
+        const double pm = A.t[0][(int64_t)u * K + a], qm = A.t[1][(int64_t)i * K + a];
+        const double pg = A.t[2][(int64_t)u * K + a], qg = A.t[3][(int64_t)i * K + a];
+        const double w3g = (double)W3[H + a];
+        vu[a] = su;
+        vi[a] = si;
+        vu[K + a] = w3g * qg;        // d r / d Pg_u = W3g * Qg_i
+        vi[K + a] = w3g * pg;        // d r / d Qg_i = W3g * Pg_u
+        thu[a] = pm;
+        thu[K + a] = pg;
+        thi[a] = qm;
+        thi[K + a] = qg;
+        gmf = fma(w3g * pg, qg, gmf);
+      }
+      rhat = bsum256(mlp + gmf, red) + (double)A.t[9][0];
+    }
+    if (tid == 0) {
+      double cdup, rsum;
+      A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
+      qw[0] = (double)n;
+      qw[1] = cdup;
+      qw[2] = cdup * rhat - rsum;
+      qw[3] = rhat;
+      qw[4] = cdup > 0.0 ? 1.0 : 0.0;
+      if (cdup > 0.0) {
+        const int s = atomicAdd(cpllist, 1);
+        cpllist[1 + s] = (int32_t)q;
+      } else {
+        const int s = atomicAdd(syslist, 2);
+        syslist[1 + s] = (int32_t)(2 * q);
+        syslist[2 + s] = (int32_t)(2 * q + 1);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Blocked left-looking LDL^T + solve, one 256-thread workgroup per system (persistent
+// over the list).  System = one side block (CPL = false, NP = NPs) or a full coupled
+// query (CPL = true, NP = 2 NPs).  Augmented matrix rows: [0, NP) the Hessian, NP the
+// right-hand side v^T, NP+1..NP+15 zero, so row NP of L is y = D^-1 L^-1 v.
+// L (column-major, LDR = NP + 16 rows) lives in this workgroup's scratch slab; panel
+// (NB columns x all rows below) in LDS.
+// ------------------------------------------------------------------------------------
+constexpr int kSolveMG = 4;   // row tiles per wave per MFMA pass
+
+template <int NP>
+constexpr int solve_nb() {
+  return ((NP + 16) * 33 + NP + 64) * 8 <= 160 * 1024 ? 32 : 16;
+}
+template <int NP>
+constexpr size_t solve_lds() {
+  return (size_t)((NP + 16) * (solve_nb<NP>() + 1) + NP + 64) * 8;
+}
+
+template <class M, int NP, bool CPL>
+__global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __restrict__ list,
+                                                   const double* __restrict__ qwork, double* __restrict__ lscr,
+                                                   double* __restrict__ xb, double* __restrict__ rec) {
+  constexpr int K = M::K, NPs = M::NPs, Ds = M::Ds, NB = solve_nb<NP>(), LDR = NP + 16, LDP = NB + 1;
+  constexpr int NRT = LDR / 16, NCT = NB / 16, MG = kSolveMG;
+  constexpr int64_t GW = gram_words<M>();
+  __shared__ double P[LDR * LDP];
+  __shared__ double dd[NP];
+  __shared__ double red[64];
+  double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * LDR * NP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ml = lane & 15, kl = lane >> 4;
+  const int nsys = list[0];
+  for (int w = blockIdx.x; w < nsys; w += gridDim.x) {
+    const int code = list[1 + w];
+    const int64_t q = CPL ? code : (code >> 1);
+    const int sd = CPL ? 0 : (code & 1);
+    const double* __restrict__ qw = qwork + q * M::QW;
+    const double s2n = 2.0 / qw[0], cdup = qw[1], esum = qw[2];
+    const double* __restrict__ vv = qw + 8 + (CPL ? 0 : sd * NPs);   // v of this system
+    const int32_t u = A.qu[q], i = A.qi[q];
+    const double* __restrict__ G0 = A.gram[0] + (int64_t)u * GW;
+    const double* __restrict__ G1 = A.gram[1] + (int64_t)i * GW;
+    auto aorig = [&](int r, int c) -> double {
+      if (r >= NP) return r == NP ? vv[c] : 0.0;
+      if constexpr (!CPL) {
+        if (r >= Ds || c >= Ds) return r == c ? 1.0 : 0.0;
+        double h = s2n * gram_at<M>(sd ? G1 : G0, r, c);
+        if (r == c) h += (M::decayed(r) ? A.wd : 0.0) + A.damping;
+        return h;
+      } else {
+        const int sr = r >= NPs, sc = c >= NPs, rr = r - sr * NPs, cc = c - sc * NPs;
+        if (rr >= Ds || cc >= Ds) return r == c ? 1.0 : 0.0;
+        double h;
+        if (sr == sc) {
+          h = s2n * (gram_at<M>(sr ? G1 : G0, rr, cc) + cdup * vv[r] * vv[c]);
+          if (r == c) h += (M::decayed(rr) ? A.wd : 0.0) + A.damping;
+        } else {
+          // item row / user column: 2 (cdup g_i g_u^T + esum d2r / dtheta_i dtheta_u)
+          const int iu = sr ? cc : rr, ii = sr ? rr : cc;
+          h = s2n * 2.0 * cdup * vv[NPs + ii] * vv[iu];
+          if (ii == iu) {
+            if constexpr (!M::ncf) {
+              if (iu < K) h += s2n * 2.0 * esum;                                     // d2 r / dp_u dq_i = I
+            } else {
+              if (iu >= K) h += s2n * 2.0 * esum * (double)A.t[8][M::H + (iu - K)];    // diag(W3g)
+            }
+          }
+        }
+        return h;
+      }
+    };
+    for (int c0 = 0; c0 < NP; c0 += NB) {
+      const int rt0 = c0 >> 4, nrt = NRT - rt0;
+      // (a) panel rows [c0, LDR) x cols [c0, c0 + NB): A - L[:, :c0] D L[c0:c0+NB, :c0]^T
+      for (int gb = wave * MG; gb < nrt; gb += 4 * MG) {
+        d4_t acc[MG][NCT];
+#pragma unroll
+        for (int m = 0; m < MG; ++m)
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              acc[m][ct][r] = gb + m < nrt ? aorig(16 * (rt0 + gb + m) + kl + 4 * r, c0 + 16 * ct + ml) : 0.0;
+#pragma unroll 2
+        for (int kk = 0; kk < c0; kk += 4) {
+          const int kc = kk + kl;
+          const double* __restrict__ Lc = Ls + (int64_t)kc * LDR;
+          const double dk = dd[kc];
+          double b[NCT], a[MG];
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) b[ct] = Lc[c0 + 16 * ct + ml] * dk;
+#pragma unroll
+          for (int m = 0; m < MG; ++m) a[m] = gb + m < nrt ? -Lc[16 * (rt0 + gb + m) + ml] : 0.0;
+#pragma unroll
+          for (int m = 0; m < MG; ++m)
+            if (gb + m < nrt)
+#pragma unroll
+              for (int ct = 0; ct < NCT; ++ct) acc[m][ct] = mfma4(a[m], b[ct], acc[m][ct]);
+        }
+#pragma unroll
+        for (int m = 0; m < MG; ++m)
+          if (gb + m < nrt)
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) P[(16 * (gb + m) + kl + 4 * r) * LDP + 16 * ct + ml] = acc[m][ct][r];
+      }
+      __syncthreads();
+      // (b) factor the panel in LDS, one thread per row (right-looking inside the panel)
+      const int prow = LDR - c0;
+      for (int j = 0; j < NB; ++j) {
+        const double dc = P[j * LDP + j];
+        for (int rr = j + 1 + tid; rr < prow; rr += 256) {
+          double* __restrict__ Pr = P + rr * LDP;
+          const double f = Pr[j] / dc;
+          const int jm = rr + 1 < NB ? rr + 1 : NB;
+          for (int jj = j + 1; jj < jm; ++jj) Pr[jj] = fma(-f, P[jj * LDP + j], Pr[jj]);
+        }
+        __syncthreads();
+      }
+      if (tid < NB) dd[c0 + tid] = P[tid * LDP + tid];
+      __syncthreads();
+      // (c) L columns of the panel (rows below the diagonal, v row included)
+      for (int j = 0; j < NB; ++j) {
+        const int c = c0 + j;
+        const double inv = 1.0 / dd[c];
+        double* __restrict__ Lc = Ls + (int64_t)c * LDR;
+        for (int r = c + 1 + tid; r < LDR; r += 256) Lc[r] = P[(r - c0) * LDP + j] * inv;
+      }
+      __syncthreads();
+    }
+    // backward solve L^T x = y, y_c = L[NP][c]; 16-column blocks from the end
+    double* __restrict__ xs = P;
+    for (int bt = NP / 16 - 1; bt >= 0; --bt) {
+      const int cb = 16 * bt;
+      for (int cc = wave; cc < 16; cc += 4) {
+        const double* __restrict__ Lc = Ls + (int64_t)(cb + cc) * LDR;
+        double acc = 0.0;
+        for (int r = cb + 16 + lane; r < NP; r += 64) acc = fma(Lc[r], xs[r], acc);
+        acc = wsum(acc);
+        if (lane == 0) red[cc] = acc;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        double val = lane < 16 ? Ls[(int64_t)(cb + lane) * LDR + NP] - red[lane] : 0.0;
+        for (int rl = 15; rl >= 0; --rl) {
+          const double xr = __shfl(val, rl);
+          if (lane < rl) val = fma(-Ls[(int64_t)(cb + lane) * LDR + cb + rl], xr, val);
+        }
+        if (lane < 16) xs[cb + lane] = val;
+      }
+      __syncthreads();
+    }
+    // epilogue: padded solution, per-side partial sums and the scoring record
+    double* __restrict__ R = rec + q * M::R;
+    for (int s = 0; s < (CPL ? 2 : 1); ++s) {
+      const int side = CPL ? s : sd;
+      const double* __restrict__ xsd = xs + (CPL ? s * NPs : 0);
+      const double* __restrict__ vsd = qw + 8 + side * NPs;
+      const double* __restrict__ th = qw + 8 + 2 * NPs + side * NPs;
+      double* __restrict__ xo = xb + q * 2 * NPs + side * NPs;
+      double cq = 0.0, xv = 0.0;
+      for (int a = tid; a < NPs; a += 256) {
+        const double xa = xsd[a];
+        xo[a] = xa;
+        if (a < Ds) {
+          if (M::decayed(a)) cq = fma(xa, th[a], cq);
+          xv = fma(xa, vsd[a], xv);
+        }
+      }
+      cq = bsum256(cq, red);
+      xv = bsum256(xv, red);
+      double* __restrict__ S = R + 8 + side * M::SB;
+      if (tid == 0) {
+        R[4 + 2 * side] = A.wd * cq;
+        R[5 + 2 * side] = xv;
+      }
+      if constexpr (!M::ncf) {
+        for (int a = tid; a <= K; a += 256) S[a] = xsd[a];
+        if (tid == 0) S[K + 1] = (double)(side ? u : i);
+      } else {
+        const float* __restrict__ W1 = A.t[4];
+        for (int c = tid; c < K; c += 256) {
+          double y = 0.0;
+          for (int a = 0; a < K; ++a) y = fma(xsd[a], (double)W1[(int64_t)(side * K + a) * K + c], y);
+          S[c] = y;
+          S[K + c] = (double)A.t[8][M::H + c] * xsd[K + c];
+        }
+        if (tid == 0) S[2 * K] = (double)(side ? u : i);
+      }
+    }
+    __syncthreads();   // xs / dd / P are rewritten by the next system
+  }
+}
+
+// per-query record header and x in the reference theta order
+template <class M>
+__global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __restrict__ qwork,
+                                                   const double* __restrict__ xb, double* __restrict__ rec,
+                                                   double* __restrict__ x_out) {
+  constexpr int Ds = M::Ds, NPs = M::NPs, D = 2 * Ds;
+  for (int64_t q = blockIdx.x; q < Q; q += gridDim.x) {
+    const double n = qwork[q * M::QW];
+    double* R = rec + q * M::R;
+    if (threadIdx.x == 0) {
+      R[0] = n > 0.0 ? 1.0 / n : NAN;
+      if (n > 0.0) {
+        R[1] = R[4] + R[6];
+        R[2] = R[5] + R[7];
+        R[3] = qwork[q * M::QW + 3];
+      }
+    }
+    if (x_out)
+      for (int a = threadIdx.x; a < D; a += 64) {
+        const int side = a >= Ds, aa = a - side * Ds;
+        x_out[q * D + M::ref_index(side, aa)] = n > 0.0 ? xb[q * 2 * NPs + side * NPs + aa] : NAN;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Entity-shared scoring (work items from build_groups: one <= kChunk chunk of one
+// entity's list x one block of <= kQueryBlock queries with that entity).  Per rating:
+//   MF  s_q = x_emb,q . emb_other + x_bias,q
+//   NCF s_q = (W1_s^T x_mlp,q) . d1_j + (W3g * x_gmf,q) . gmf_other
+//   influence = (2 e_j s_q + c_q) / n_q   (mf:240-246); the test pair's own train row
+//   takes e and s = x.v from the record (bit-identical copies).
+// ------------------------------------------------------------------------------------
+template <class M>
+constexpr int score_waves() {
+  return (4 + M::SB) * kQueryBlock * 8 > 20000 ? 2 : 4;
+}
+
+template <class M>
+__global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
+    BigArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
+    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  constexpr int K = M::K, SW = score_waves<M>(), QB = kQueryBlock, RSW = 4 + M::SB;
+  constexpr int NPASS = kScoreRows;
+  __shared__ double srec[SW][QB * RSW];
+  __shared__ int64_t sbase[SW][3 * QB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_items = wstart[nE];
+  const int64_t stride = (int64_t)gridDim.x * SW;
+  for (int64_t wi = (int64_t)blockIdx.x * SW + wave; wi < n_items; wi += stride) {
+    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int sd = g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(g - A.U) : g;
+    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
+    const int64_t gn = gstart[g + 1] - gb;
+    const int nq = gn < QB ? (int)gn : QB;
+    const int32_t* __restrict__ oth = A.other[sd] + lb;
+    const float* __restrict__ rat = A.rating[sd] + lb;
+    const int32_t* __restrict__ rw = A.row[sd] + lb;
+    const float* __restrict__ T = M::ncf ? (sd == 0 ? A.t[3] : A.t[2]) : (sd == 0 ? A.t[1] : A.t[0]);
+    double* __restrict__ rl = srec[wave];
+    int64_t* __restrict__ bl = sbase[wave];
+    __builtin_amdgcn_wave_barrier();
+    for (int t = lane; t < QB * RSW; t += 64) {
+      const int j = t / RSW, c = t - j * RSW;
+      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
+      rl[t] = rec[(int64_t)q * M::R + (c < 4 ? c : 8 + sd * M::SB + (c - 4))];
+    }
+    if (lane < QB) {
+      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
+      const int64_t* qb = qbase + 4 * (int64_t)q;
+      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
+      bl[QB + lane] = qb[2 + sd] + cidx;
+      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (int h = 0; h < NPASS; ++h) {
+      const int idx = h * 64 + lane;
+      const bool ok = idx < len;
+      const int li = ok ? idx : 0;
+      const int32_t o = oth[li], row = rw[li];
+      const float y = rat[li];
+      const double ej = A.resid[row];
+      double s[QB];
+#pragma unroll
+      for (int j = 0; j < QB; ++j) s[j] = 0.0;
+      const float4* __restrict__ src = reinterpret_cast<const float4*>(T + (int64_t)o * K);
+      constexpr int OFF_B = M::ncf ? K : 0;   // record offset of the vector dotted with the gathered row
+#pragma unroll 2
+      for (int c4 = 0; c4 < K / 4; c4 += 2) {
+        const float4 v0 = src[c4], v1 = src[c4 + 1];
+        const double g8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int j = 0; j < QB; ++j) {
+          if (j >= nq) break;
+          const double* xr = rl + j * RSW + 4 + OFF_B + 4 * c4;
+#pragma unroll
+          for (int cc = 0; cc < 8; ++cc) s[j] = fma(xr[cc], g8[cc], s[j]);
+        }
+      }
+      if constexpr (M::ncf) {
+        const double2* __restrict__ dsrc = reinterpret_cast<const double2*>(A.d1 + (int64_t)row * K);
+#pragma unroll 2
+        for (int c2 = 0; c2 < K / 2; c2 += 2) {
+          const double2 a0 = dsrc[c2], a1 = dsrc[c2 + 1];
+          const double g4[4] = {a0.x, a0.y, a1.x, a1.y};
+#pragma unroll
+          for (int j = 0; j < QB; ++j) {
+            if (j >= nq) break;
+            const double* yr = rl + j * RSW + 4 + 2 * c2;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) s[j] = fma(yr[cc], g4[cc], s[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        if (j >= nq) break;
+        const double* __restrict__ Rj = rl + j * RSW;
+        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat = Rj[3];
+        double ss = s[j], ee = ej;
+        double dup;
+        if constexpr (!M::ncf) {
+          ss += Rj[4 + K];
+          dup = Rj[4 + K + 1];
+        } else {
+          dup = Rj[4 + 2 * K];
+        }
+        if ((double)o == dup) { ee = rhat - (double)y; ss = xv; }
+        const double infl = (2.0 * ee * ss + cq) * inv_n;
+        const int64_t obj = bl[j];
+        if (ok) {
+          if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
+          if (rel_idx) __builtin_nontemporal_store((int64_t)row, rel_idx + obj + idx);
+        }
+        if (K_top > 0) {
+          const int64_t cbj = bl[QB + j];
+          const int64_t poj = bl[2 * QB + j];
+          const double la = ok ? topk_key(infl) : -2.0;
+          const int lp = ok ? cidx * kChunk + idx : -1;
+          double pa = INFINITY;
+          int pp = -1;
+          for (int t = 0; t < K_top; ++t) {
+            double ba = -2.0, bv = 0.0;
+            int bp = 0x7fffffff;
+            if (lp >= 0 && better(pa, pp, la, lp)) { ba = la; bp = lp; bv = infl; }
+            wave_best(ba, bp, bv);
+            if (lane == 0) {
+              const bool okk = ba > -1.5;
+              const int64_t slot = (cbj * NPASS + h) * K_top + t;
+              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+              cand_val[slot] = okk ? bv : NAN;
+            }
+            pa = ba;
+            pp = bp;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------
+BigArgs make_big_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
+  BigArgs A;
+  A.qu = qu;
+  A.qi = qi;
+  A.U = c->p.U;
+  A.I = c->p.I;
+  for (int s = 0; s < 2; ++s) {
+    A.ptr[s] = c->idx.side[s].ptr.as<int64_t>();
+    A.row[s] = c->idx.side[s].row.as<int32_t>();
+    A.other[s] = c->idx.side[s].other.as<int32_t>();
+    A.rating[s] = c->idx.side[s].rating.as<float>();
+    A.gram[s] = c->gram[s].as<double>();
+    A.l1[s] = c->l1[s].as<double>();
+  }
+  A.resid = c->resid.as<double>();
+  A.d1 = c->d1.as<double>();
+  for (int t = 0; t < 10; ++t) A.t[t] = c->p.t[t];
+  A.wd = c->p.wd;
+  A.damping = c->p.damping;
+  A.pairs.key = c->idx.pkey.as<unsigned long long>();
+  A.pairs.cnt = c->idx.pcnt.as<int32_t>();
+  A.pairs.sum = c->idx.psum.as<double>();
+  A.pairs.mask = (unsigned long long)(c->idx.pcap - 1);
+  return A;
+}
+
+inline unsigned grid_cap(int64_t n, int64_t cap) {
+  if (n < 1) n = 1;
+  return (unsigned)(n < cap ? n : cap);
+}
+
+int cu_count(fia_ctx* c) {
+  if (c->num_cus <= 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || n <= 0) n = 256;
+    c->num_cus = n;
+  }
+  return c->num_cus;
+}
+
+// Gram work lists for the current index: slices of <= kBigSlice ratings, longest lists
+// first; split lists get partial slots summed by k_big_combine in slot order.
+hipError_t big_work_lists(fia_ctx* c) {
+  Index& X = c->idx;
+  if (c->bitems_version == X.version) return hipSuccess;
+  for (int sd = 0; sd < 2; ++sd) {
+    const std::vector<int64_t>& hp = X.hptr[sd];
+    const int64_t ne = (int64_t)hp.size() - 1;
+    std::vector<int32_t> ord((size_t)ne);
+    for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = (int32_t)e;
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+      return hp[(size_t)a + 1] - hp[(size_t)a] > hp[(size_t)b + 1] - hp[(size_t)b];
+    });
+    std::vector<int32_t> items, comb;
+    int32_t slots = 0;
+    for (int32_t e : ord) {
+      const int64_t len = hp[(size_t)e + 1] - hp[(size_t)e];
+      const int64_t nit = len == 0 ? 1 : (len + kBigSlice - 1) / kBigSlice;
+      if (nit > 1) comb.insert(comb.end(), {e, slots, (int32_t)nit, 0});
+      for (int64_t t = 0; t < nit; ++t) {
+        const int64_t st = t * kBigSlice;
+        const int64_t ln = std::min<int64_t>(kBigSlice, len - st);
+        items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), nit > 1 ? slots++ : -1});
+      }
+    }
+    c->n_bitems[sd] = (int64_t)items.size() / 4;
+    c->n_bcomb[sd] = (int64_t)comb.size() / 4;
+    c->n_bslots[sd] = slots;
+    FIA_HIP_TRY(c->bitems[sd].reserve(sizeof(int32_t) * items.size()));
+    FIA_HIP_TRY(hipMemcpy(c->bitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+    if (!comb.empty()) {
+      FIA_HIP_TRY(c->bcomb[sd].reserve(sizeof(int32_t) * comb.size()));
+      FIA_HIP_TRY(hipMemcpy(c->bcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
+    }
+  }
+  c->bitems_version = X.version;
+  return hipSuccess;
+}
+
+template <class M>
+hipError_t prepare_big_impl(fia_ctx* c, hipStream_t s) {
+  constexpr int K = M::K;
+  constexpr int64_t GW = gram_words<M>();
+  Index& X = c->idx;
+  const int64_t N = X.N;
+  const int64_t n_ent[2] = {c->p.U, c->p.I};
+  const unsigned gN = grid_cap((N + 255) / 256, 16384);
+  if (c->self_version != X.version) {
+    for (int sd = 0; sd < 2; ++sd) {
+      FIA_HIP_TRY(c->self[sd].reserve(sizeof(int32_t) * (size_t)(N + 1)));
+      if (N > 0) {
+        hipLaunchKernelGGL(k_self, dim3(gN), dim3(256), 0, s, N, n_ent[sd], X.side[sd].ptr.as<int64_t>(),
+                           c->self[sd].as<int32_t>());
+        FIA_HIP_TRY(hipGetLastError());
+      }
+    }
+    c->self_version = X.version;
+  }
+  FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(N + 1)));
+  if constexpr (!M::ncf) {
+    if (N > 0) {
+      hipLaunchKernelGGL(k_resid_mf<K>, dim3(gN), dim3(256), 0, s, N, c->self[0].as<int32_t>(),
+                         X.side[0].other.as<int32_t>(), X.side[0].row.as<int32_t>(), X.side[0].rating.as<float>(),
+                         c->p.t[0], c->p.t[1], c->p.t[2], c->p.t[3], c->p.t[4], c->resid.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+  } else {
+    for (int sd = 0; sd < 2; ++sd) {
+      FIA_HIP_TRY(c->l1[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * K + 1)));
+      hipLaunchKernelGGL(k_l1_big<K>, dim3(grid_cap((n_ent[sd] * K + 255) / 256, 16384)), dim3(256), 0, s,
+                         c->p.t[sd], c->p.t[4], sd * K, n_ent[sd], c->l1[sd].as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+    FIA_HIP_TRY(c->d1.reserve(sizeof(double) * (size_t)(N * K + 1)));
+    if (N > 0) {
+      hipLaunchKernelGGL(k_ncf_rows<K>, dim3(grid_cap((N + 15) / 16, 65536)), dim3(64), 0, s, N,
+                         c->self[0].as<int32_t>(), X.side[0].other.as<int32_t>(), X.side[0].row.as<int32_t>(),
+                         X.side[0].rating.as<float>(), c->l1[0].as<double>(), c->l1[1].as<double>(), c->p.t[5],
+                         c->p.t[6], c->p.t[7], c->p.t[8], c->p.t[9], c->p.t[2], c->p.t[3], c->d1.as<double>(),
+                         c->resid.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+  }
+  FIA_HIP_TRY(big_work_lists(c));
+  for (int sd = 0; sd < 2; ++sd) {
+    FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * GW)));
+    if (c->n_bslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(c->n_bslots[sd] * GW)));
+    const float* emb_other = M::ncf ? c->p.t[sd == 0 ? 3 : 2] : c->p.t[sd == 0 ? 1 : 0];
+    if (c->n_bitems[sd] > 0) {
+      hipLaunchKernelGGL(k_big_gram<M>, dim3(grid_cap(c->n_bitems[sd], 1 << 20), GramCfg<M>::NG), dim3(64 * kGW), 0, s,
+                         sd, c->n_bitems[sd], c->bitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(),
+                         X.side[sd].other.as<int32_t>(), X.side[sd].row.as<int32_t>(), emb_other,
+                         c->d1.as<double>(), c->p.t[4], c->p.t[8], c->gram[sd].as<double>(),
+                         c->gpart[sd].as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+    if (c->n_bcomb[sd] > 0) {
+      hipLaunchKernelGGL(k_big_combine, dim3(grid_cap(c->n_bcomb[sd], 65536)), dim3(256), 0, s, c->n_bcomb[sd],
+                         c->bcomb[sd].as<int32_t>(), GW, c->gpart[sd].as<double>(), c->gram[sd].as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+  }
+  return hipSuccess;
+}
+
+template <class M, int NP, bool CPL>
+hipError_t launch_solve(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int32_t* list, hipStream_t s) {
+  if (max_sys <= 0) return hipSuccess;
+  constexpr size_t lds = solve_lds<NP>();
+  const int per_cu = (int)((160 * 1024) / lds);
+  const int64_t resident = (int64_t)cu_count(c) * (per_cu > 0 ? per_cu : 1);
+  const int64_t grid = max_sys < resident ? max_sys : resident;
+  constexpr int64_t slab = (int64_t)(NP + 16) * NP;
+  FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(grid * slab)));
+  hipLaunchKernelGGL((k_big_solve<M, NP, CPL>), dim3((unsigned)grid), dim3(256), 0, s, A, list,
+                     c->qwork.as<double>(), c->lscr.as<double>(), c->xb.as<double>(), c->rec.as<double>());
+  return hipGetLastError();
+}
+
+template <class M>
+hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                          int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                          int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+  constexpr int NPs = M::NPs, NPASS = kScoreRows, SW = score_waves<M>();
+  FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));
+  FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * M::QW + 1)));
+  FIA_HIP_TRY(c->xb.reserve(sizeof(double) * (size_t)(Q * 2 * NPs + 1)));
+  FIA_HIP_TRY(c->syslist.reserve(sizeof(int32_t) * (size_t)(2 * Q + 2)));
+  FIA_HIP_TRY(c->cpllist.reserve(sizeof(int32_t) * (size_t)(Q + 2)));
+  if (K > 0) {
+    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * NPASS)));
+    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * NPASS)));
+  }
+  const BigArgs A = make_big_args(c, qu, qi);
+  phase_begin(c, 4, s);
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, true, s));
+  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, s));
+  phase_end(c, 4, s);
+  phase_begin(c, 1, s);
+  FIA_HIP_TRY(hipMemsetAsync(c->syslist.ptr, 0, sizeof(int32_t), s));
+  FIA_HIP_TRY(hipMemsetAsync(c->cpllist.ptr, 0, sizeof(int32_t), s));
+  hipLaunchKernelGGL(k_big_prologue<M>, dim3(grid_cap(Q, 1 << 20)), dim3(256), 0, s, A, Q, c->qwork.as<double>(),
+                     c->syslist.as<int32_t>(), c->cpllist.as<int32_t>());
+  FIA_HIP_TRY(hipGetLastError());
+  FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+  FIA_HIP_TRY((launch_solve<M, 2 * NPs, true>(c, A, Q, c->cpllist.as<int32_t>(), s)));
+  hipLaunchKernelGGL(k_big_finish<M>, dim3(grid_cap(Q, 1 << 20)), dim3(64), 0, s, Q, c->qwork.as<double>(),
+                     c->xb.as<double>(), c->rec.as<double>(), x_out);
+  FIA_HIP_TRY(hipGetLastError());
+  phase_end(c, 1, s);
+  phase_begin(c, 2, s);
+  hipLaunchKernelGGL(k_big_score<M>, dim3(grid_cap((max_chunks + SW - 1) / SW, 8192)), dim3(64 * SW), 0, s, A,
+                     c->p.U + c->p.I, c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                     c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                     c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+  FIA_HIP_TRY(hipGetLastError());
+  phase_end(c, 2, s);
+  if (K > 0) {
+    phase_begin(c, 3, s);
+    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, NPASS, topk_pos, topk_idx, topk_val, s));
+    phase_end(c, 3, s);
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
+#define FIA_BIG_CASES(X) \
+  X(FIA_MODEL_MF, 128, BMF<128>) X(FIA_MODEL_MF, 256, BMF<256>) X(FIA_MODEL_NCF, 64, BNCF<64>) \
+  X(FIA_MODEL_NCF, 128, BNCF<128>) X(FIA_MODEL_NCF, 256, BNCF<256>)
+
+bool big_supported(int model, int k) {
+#define X(m, kk, T) if (model == m && k == kk) return true;
+  FIA_BIG_CASES(X)
+#undef X
+  return false;
+}
+
+hipError_t prepare_big(fia_ctx* c, hipStream_t s) {
+#define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_big_impl<T>(c, s);
+  FIA_BIG_CASES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                     int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+#define X(m, kk, T)                                                                                            \
+  if (c->p.model == m && c->p.k == kk)                                                                         \
+    return query_big_impl<T>(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos, topk_idx, \
+                             topk_val, s);
+  FIA_BIG_CASES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+}  // namespace fia

@@ -84,6 +84,8 @@ struct Index {
   DevBuf pcnt;    // int32  [pcap]
   DevBuf psum;    // double [pcap]
   int64_t pcap = 0;
+  std::vector<int64_t> hptr[2];   // host copies of side[s].ptr (large-k Gram work lists)
+  uint64_t version = 0;           // bumped by every build_index
   bool valid = false;
 };
 
@@ -162,6 +164,22 @@ struct fia_ctx {
   fia::DevBuf wcnt;       // int64 [U + I + 1] work items per entity -> scan in wstart
   fia::DevBuf wstart;     // int64 [U + I + 1]
   fia::DevBuf witems;     // int32 [3 * max items] {global entity, list chunk, query block}
+  // large-k path (bigk.hip): per-list-position entity, per-train-row residual / NCF backward
+  // vectors, per-query Hessian inputs and solutions, solve lists and LDL^T scratch
+  fia::DevBuf self[2];    // int32 [N] entity owning list position p of side s
+  uint64_t self_version = ~0ull;
+  fia::DevBuf resid;      // double [N]   e_j = r-hat_j - y_j by train row
+  fia::DevBuf d1;         // double [N*k] NCF masked backward vector by train row
+  fia::DevBuf bitems[2], bcomb[2];   // large-k Gram work lists {entity, start, len, slot}
+  int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0};
+  uint64_t bitems_version = ~0ull;
+  int bitems_k = 0;
+  fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta
+  fia::DevBuf xb;         // double [Q * 2 NPs] per-query solution (padded side blocks)
+  fia::DevBuf syslist;    // int32 [1 + 2Q] {count, 2q + side ...} uncoupled side systems
+  fia::DevBuf cpllist;    // int32 [1 + Q]  {count, q ...} coupled full systems
+  fia::DevBuf lscr;       // double LDL^T factor scratch, one slab per resident solve workgroup
+  int num_cus = 0;
   bool score_grouped = false;   // scoring schedule, see fia_create
   bool profiling = false;
   fia::PhaseEvents events;
@@ -192,6 +210,16 @@ hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
                        bool& unsupported);
 int model_num_params(int model, int k);
 bool model_supported(int model, int k);
+
+// large-k models (bigk.hip): MF k in {128, 256}, NCF k in {64, 128, 256}
+bool big_supported(int model, int k);
+hipError_t prepare_big(fia_ctx* c, hipStream_t s);
+hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                     int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);
+// per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
+hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
+                             int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);
 
 // phase event helpers (no-ops unless profiling)
 void phase_begin(fia_ctx* c, int phase, hipStream_t s);

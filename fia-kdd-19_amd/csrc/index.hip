@@ -296,6 +296,7 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
     std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
       return hptr[(size_t)a + 1] - hptr[(size_t)a] > hptr[(size_t)b + 1] - hptr[(size_t)b];
     });
+    X.hptr[sd] = hptr;
     FIA_HIP_TRY(X.order[sd].reserve(sizeof(int32_t) * ord.size()));
     FIA_HIP_TRY(hipMemcpy(X.order[sd].ptr, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice));
     // Gram work items (longest lists first) and the combine list of split entities
@@ -340,6 +341,7 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
   }
   FIA_HIP_TRY(hipStreamSynchronize(s));
   X.pcap = cap;
+  ++X.version;
   X.N = N;
   X.U = U;
   X.I = I;

@@ -1745,7 +1745,17 @@ bool model_supported(int model, int k) {
 #define X(m, kk, T) if (model == m && k == kk) return true;
   FIA_MODEL_CASES(X)
 #undef X
-  return false;
+  return big_supported(model, k);
+}
+
+hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
+                             int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+  if (K <= 0 || Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)Q), dim3(64), 0, s, qu, qi, Q, c->coff.as<int64_t>(), K, spc,
+                     c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), c->idx.side[0].ptr.as<int64_t>(),
+                     c->idx.side[0].row.as<int32_t>(), c->idx.side[1].ptr.as<int64_t>(),
+                     c->idx.side[1].row.as<int32_t>(), c->p.U, c->p.I, topk_pos, topk_idx, topk_val);
+  return hipGetLastError();
 }
 
 int model_num_params(int model, int k) {
@@ -1759,6 +1769,7 @@ hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported) {
 #define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_impl<T>(c, s);
   FIA_MODEL_CASES(X)
 #undef X
+  if (big_supported(c->p.model, c->p.k)) return prepare_big(c, s);
   unsupported = true;
   return hipSuccess;
 }
@@ -1773,6 +1784,9 @@ hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
                          topk_val, s);
   FIA_MODEL_CASES(X)
 #undef X
+  if (big_supported(c->p.model, c->p.k))
+    return query_big(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos, topk_idx, topk_val,
+                     s);
   unsupported = true;
   return hipSuccess;
 }

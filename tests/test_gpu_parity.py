@@ -262,3 +262,43 @@ def test_invalid_queries_raise(tmp_path):
         m.get_influence_batch([1], K=1)
     with pytest.raises(FIAError):
         m.get_influence_batch([0], K=65)
+
+
+@pytest.mark.parametrize("model,k", [("MF", 128), ("MF", 256), ("NCF", 64), ("NCF", 128), ("NCF", 256)])
+def test_large_k_matches_oracle(model, k, tmp_path):
+    """The large-k path (tile-packed Gram caches, blocked MFMA LDL^T, entity-shared
+    scoring): a long item list (Gram slices + partial combine, 3 scoring chunks), a
+    query group of > 8 queries on that item (several query blocks), the pair in
+    train twice (coupled full-D solve), an empty user side."""
+    from oracle import fia_oracle as fo
+    rng = np.random.default_rng(k + (100 if model == "NCF" else 0))
+    U, I, N = 2600, 30, 6000
+    key = np.sort(rng.choice((U - 1) * (I - 1), N, replace=False))
+    tu, ti = (key // (I - 1)).astype(np.int32), (key % (I - 1)).astype(np.int32)
+    # item I-1 rated by 2200 users (two Gram slices, 9 scoring chunks); pair (tu[5], ti[5]) twice more
+    ex = rng.choice(U - 1, 2200, replace=False).astype(np.int32)
+    tu = np.concatenate([tu, ex, [tu[5], tu[5]]]).astype(np.int32)
+    ti = np.concatenate([ti, np.full(ex.size, I - 1, np.int32), [ti[5], ti[5]]]).astype(np.int32)
+    tr = rng.integers(1, 6, tu.size).astype(np.float32)
+    p = synth.mf_params(U, I, k, 3) if model == "MF" else synth.ncf_params(U, I, k, 3)
+    shared = [(int(u), I - 1) for u in rng.choice(U - 1, 11, replace=False)]
+    qs = [(1, 2), (int(tu[5]), int(ti[5])), (U - 1, 3), (7, I - 1), (U - 1, I - 1), (int(ex[0]), I - 1)] + shared
+    qu = np.array([q[0] for q in qs], np.int32)
+    qi = np.array([q[1] for q in qs], np.int32)
+    m = make_model(model, U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    res = m.get_influence_batch(list(range(len(qs))), K=3)
+    for q, (u, i) in enumerate(qs):
+        o = fo.query(model, p, k, tu, ti, tr, u, i, 1e-3, 1e-6)
+        b, e = res["offsets"][q], res["offsets"][q + 1]
+        assert np.array_equal(o["rel"], res["rel_idx"][b:e])
+        if o["n"]:
+            assert rel_err(res["influence"][b:e], o["influence"]) < RTOL, (model, k, q)
+            assert rel_err(res["x"][q], o["x"]) < RTOL, (model, k, q)
+            check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], 3)
+        else:
+            assert np.isnan(res["x"][q]).all()
+    # the two copies of a train row in rel carry identical bits
+    b, e = res["offsets"][1], res["offsets"][2]
+    rel, infl = res["rel_idx"][b:e], res["influence"][b:e]
+    for row in np.unique(rel[np.bincount(rel)[rel] > 1]):
+        assert (infl[rel == row] == infl[rel == row][0]).all()
