@@ -35,6 +35,10 @@ CONFIGS = {
     "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp"),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
                      k=64, data="20m"),
+    "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "
+                      "blocks per query)", model="MF", k=256, data="20m"),
+    "20m-ncf256": dict(workload="NCF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 512^2 "
+                       "blocks per query)", model="NCF", k=256, data="20m"),
 }
 
 
@@ -47,6 +51,9 @@ def parse():
     ap.add_argument("--topk", type=int, default=1)
     ap.add_argument("--batch-rows", type=int, default=1 << 29,
                     help="max related ratings per fia_query_batch call (output buffers are reused)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="answer only this rank's 1/S share of the query set (contiguous, balanced by n_q): "
+                         "with S=8 at N=1 this is one GPU's share of the 8-GPU strong-scaling job")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
@@ -124,10 +131,9 @@ def main():
     d, params = load_data(cfg)
     tu, ti, tr = d["train"]
     qu_np, qi_np, _ = d["test"]
-    if world > 1 and rank > 0:       # same per-GPU batch, rank-rotated order
+    if world > 1 and rank > 0 and args.shard_of <= 1:   # same per-GPU batch, rank-rotated order
         shift = (rank * qu_np.size) // world
         qu_np, qi_np = np.roll(qu_np, -shift), np.roll(qi_np, -shift)
-    Q = int(qu_np.size)
     U, I, k = d["U"], d["I"], cfg["k"]
     model_id = _lib.FIA_MODEL_MF if cfg["model"] == "MF" else _lib.FIA_MODEL_NCF
 
@@ -146,6 +152,12 @@ def main():
     qi = torch.from_numpy(qi_np).to(dev)
     offsets_all, _ = ctx.count_related(qu, qi)
     n_q = np.diff(offsets_all.cpu().numpy())
+    if args.shard_of > 1:
+        from influence.sharding import shard_ranges
+        b0, b1 = shard_ranges(n_q, args.shard_of)[rank % args.shard_of]
+        qu_np, qi_np, n_q = qu_np[b0:b1], qi_np[b0:b1], n_q[b0:b1]
+        qu, qi = qu[b0:b1].contiguous(), qi[b0:b1].contiguous()
+    Q = int(qu_np.size)
     total = int(n_q.sum())
     D = ctx.num_params()
     K = args.topk
@@ -220,13 +232,13 @@ def main():
         "metric": "influence queries/sec (whole node) + % HBM roofline, MF k=16 ML-1M-ex"
         if args.config == "ml1m-mf" else "influence queries/sec (whole node), " + cfg["workload"],
         "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak" if args.shard_of <= 1 else "strong", "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic train ratings of the reference shape (train file not distributed) + the reference's "
                 "real held-out test pairs; synthetic parameters",
         "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_gpu": Q,
                    "n_train": int(tu.size), "related_ratings_per_gpu_step": int(total), "topk": K,
-                   "query_batches": len(batches),
+                   "query_batches": len(batches), "shard_of": args.shard_of,
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -550,7 +550,7 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
     const double* __restrict__ G0 = A.gram[0] + (int64_t)u * GW;
     const double* __restrict__ G1 = A.gram[1] + (int64_t)i * GW;
     auto aorig = [&](int r, int c) -> double {
-      if (r >= NP) return r == NP ? vv[c] : 0.0;
+      if (r >= NP) return (r == NP && c < NP) ? vv[c] : 0.0;
       if constexpr (!CPL) {
         if (r >= Ds || c >= Ds) return r == c ? 1.0 : 0.0;
         double h = s2n * gram_at<M>(sd ? G1 : G0, r, c);
@@ -580,6 +580,7 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
     };
     for (int c0 = 0; c0 < NP; c0 += NB) {
       const int rt0 = c0 >> 4, nrt = NRT - rt0;
+      const int nbe = NP - c0 < NB ? NP - c0 : NB;   // last panel of NP = 16 (2m+1): one tile column
       // (a) panel rows [c0, LDR) x cols [c0, c0 + NB): A - L[:, :c0] D L[c0:c0+NB, :c0]^T
       for (int gb = wave * MG; gb < nrt; gb += 4 * MG) {
         d4_t acc[MG][NCT];
@@ -617,20 +618,20 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
       __syncthreads();
       // (b) factor the panel in LDS, one thread per row (right-looking inside the panel)
       const int prow = LDR - c0;
-      for (int j = 0; j < NB; ++j) {
+      for (int j = 0; j < nbe; ++j) {
         const double dc = P[j * LDP + j];
         for (int rr = j + 1 + tid; rr < prow; rr += 256) {
           double* __restrict__ Pr = P + rr * LDP;
           const double f = Pr[j] / dc;
-          const int jm = rr + 1 < NB ? rr + 1 : NB;
+          const int jm = rr + 1 < nbe ? rr + 1 : nbe;
           for (int jj = j + 1; jj < jm; ++jj) Pr[jj] = fma(-f, P[jj * LDP + j], Pr[jj]);
         }
         __syncthreads();
       }
-      if (tid < NB) dd[c0 + tid] = P[tid * LDP + tid];
+      if (tid < nbe) dd[c0 + tid] = P[tid * LDP + tid];
       __syncthreads();
       // (c) L columns of the panel (rows below the diagonal, v row included)
-      for (int j = 0; j < NB; ++j) {
+      for (int j = 0; j < nbe; ++j) {
         const int c = c0 + j;
         const double inv = 1.0 / dd[c];
         double* __restrict__ Lc = Ls + (int64_t)c * LDR;
