@@ -183,8 +183,13 @@ def main():
     tix = torch.empty(Q * K, dtype=torch.int64, device=dev)
     tv = torch.empty(Q * K, dtype=torch.float64, device=dev)
 
+    big_k = k >= 128 or (cfg["model"] == "NCF" and k >= 64)
+
     def step():
-        ctx.prepare()
+        if big_k:
+            ctx.prepare_for(qu, qi)    # caches for this GPU's users/items only (fia_prepare_for)
+        else:
+            ctx.prepare()
         for b0, b1, qb_u, qb_i, off_b, tot_b in batches:
             ctx.count_related(qb_u, qb_i, off_b, want_total=False)
             ctx.query_batch(qb_u, qb_i, off_b, tot_b, rel, infl, xbuf, K, tp[b0 * K:b1 * K],

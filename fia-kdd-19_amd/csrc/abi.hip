@@ -106,11 +106,17 @@ int fia_destroy(fia_ctx* c) {
       c->idx.gitems[s].release();
       c->idx.gcomb[s].release();
       c->gpart[s].release();
+      c->self[s].release();
+      c->gm[s].release();
+      c->slot[s].release();
+      c->bitems[s].release();
+      c->bcomb[s].release();
     }
     fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->scan_tmp,
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
                            &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->wcnt,
-                           &c->wstart, &c->witems};
+                           &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,
+                           &c->cpllist, &c->lscr, &c->mark};
     for (auto* b : bufs) b->release();
     for (auto& v : c->events.ev)
       for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
@@ -187,8 +193,37 @@ int fia_prepare(fia_ctx* c, void* stream) {
     fia::phase_begin(c, 0, s);
     hipError_t e = fia::prepare_model(c, s, unsup);
     fia::phase_end(c, 0, s);
+    c->prepared = false;
     if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
+    if (e == hipErrorOutOfMemory) return fail(c, FIA_ERR_NOMEM, "device memory exhausted by the Hessian caches");
     if (e != hipSuccess) return hip_fail(c, e, "fia_prepare");
+    c->prepared = true;
+    return FIA_OK;
+  })
+}
+
+int fia_prepare_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  FIA_GUARDED(c, {
+    if (!c->p.valid) return fail(c, FIA_ERR_STATE, "fia_set_params has not been called");
+    if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
+    if (Q < 0 || Q >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "num_queries out of range");
+    if (Q > 0 && (!qu || !qi)) return fail(c, FIA_ERR_INVALID, "null query array");
+    DeviceGuard g(c->device);
+    hipStream_t s = as_stream(stream);
+    bool unsup = false;
+    hipError_t e;
+    fia::phase_begin(c, 0, s);
+    if (fia::big_supported(c->p.model, c->p.k)) {
+      e = fia::prepare_big(c, Q, qu, qi, s);
+    } else {
+      e = fia::prepare_model(c, s, unsup);   // small k: the caches are cheap, build them all
+    }
+    fia::phase_end(c, 0, s);
+    c->prepared = false;
+    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
+    if (e == hipErrorOutOfMemory) return fail(c, FIA_ERR_NOMEM, "device memory exhausted by the Hessian caches");
+    if (e != hipSuccess) return hip_fail(c, e, "fia_prepare_for");
     c->prepared = true;
     return FIA_OK;
   })
@@ -211,6 +246,7 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
     }
     e = fia::count_related(c, Q, qu, qi, offsets, s);
+    if (e == hipSuccess && total_out) e = fia::check_cover(c, Q, qu, qi, c->flag.as<int32_t>() + 2, s);
     if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
     if (total_out) {
       int32_t flags[4] = {0, 0, 0, 0};
@@ -219,6 +255,9 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       if (e == hipSuccess) e = hipStreamSynchronize(s);
       if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
       if (flags[1]) return fail(c, FIA_ERR_INVALID, "query ids out of range [0, num_users) x [0, num_items)");
+      if (flags[2])
+        return fail(c, FIA_ERR_STATE, "a query's user or item has no Hessian cache: it was not among the "
+                                      "queries of the last fia_prepare_for");
     }
     return FIA_OK;
   })

@@ -9,8 +9,8 @@
 // but every structure is sized for blocks that do not fit a wave's registers or a
 // CU's LDS:
 //   * per train row, once per prepare: the residual e_j = r-hat_j - y_j and (NCF) the
-//     masked MLP backward vector d1_j (k_resid_mf / k_ncf_rows, the NCF one as three
-//     f64-MFMA products per 16 ratings);
+//     restricted MLP gradient halves g_mlp,side = W1_side . d1_j of both sides
+//     (k_resid_mf / k_ncf_rows, the NCF one as four f64-MFMA products per 16 ratings);
 //   * per entity: the Gram A_e = sum g g^T in 16x16 tiles (tile-packed lower, fp64),
 //     accumulated on v_mfma_f64_16x16x4_f64 from 16-rating slabs staged in LDS
 //     (k_big_gram; long lists split into slices, partials summed in slot order);
@@ -75,7 +75,7 @@ __device__ __forceinline__ void wave_best(double& a, int& p, double& v) {
 // ------------------------------------------------------------------------------------
 // model traits.  A side block has Ds coordinates padded to NPs = 16 T.
 //   MF  side [emb (k), bias, 0 pad]  (mf:43-65)    record [x_emb (k), x_bias, dup_other]
-//   NCF side [mlp emb (k), gmf emb (k)] (ncf:49-64) record [W1_s^T x_mlp (k), W3g*x_gmf (k), dup_other]
+//   NCF side [mlp emb (k), gmf emb (k)] (ncf:49-64) record [x_mlp (k), W3g*x_gmf (k), dup_other]
 // per-query record: [1/n, c_q, x.v, r-hat(u,i), cq_u, xv_u, cq_i, xv_i, side 0, side 1]
 // per-query work:   [n, cdup, esum, r-hat, coupled, -, -, -, v_u, v_i, theta_u, theta_i]
 // ------------------------------------------------------------------------------------
@@ -122,13 +122,37 @@ struct BigArgs {
   const double* gram[2];
   const double* l1[2];
   const double* resid;
-  const double* d1;
+  const double* gm[2];     // NCF g_mlp per side, by train row
+  const int32_t* slot[2];  // Gram cache slot per entity (nullptr = identity)
   const float* t[10];
   double wd, damping;
   PairTable pairs;
 };
 
 // ------------------------------------------------------------------------------------
+// entities referenced by a query set (fia_prepare_for)
+__global__ void k_mark(int64_t Q, const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t U,
+                       int64_t I, uint8_t* __restrict__ mark) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = qu[q], i = qi[q];
+    if (u >= 0 && u < U && i >= 0 && i < I) {
+      mark[u] = 1;
+      mark[U + i] = 1;
+    }
+  }
+}
+
+__global__ void k_check_cover(int64_t Q, const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t U,
+                              int64_t I, const int32_t* __restrict__ slot0, const int32_t* __restrict__ slot1,
+                              int32_t* __restrict__ flag) {
+  int bad = 0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = qu[q], i = qi[q];
+    if (u >= 0 && u < U && i >= 0 && i < I) bad |= slot0[u] < 0 || slot1[i] < 0;
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 // per-position entity of a side's lists: self[p] = e with ptr[e] <= p < ptr[e+1]
 // ------------------------------------------------------------------------------------
 __global__ void k_self(int64_t N, int64_t n_ent, const int64_t* __restrict__ ptr, int32_t* __restrict__ self) {
@@ -192,7 +216,9 @@ __global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __res
                                                  const float* __restrict__ W2, const float* __restrict__ b2,
                                                  const float* __restrict__ W3, const float* __restrict__ b3,
                                                  const float* __restrict__ Pg, const float* __restrict__ Qg,
-                                                 double* __restrict__ d1s, double* __restrict__ resid) {
+                                                 const float* __restrict__ W1, double* __restrict__ gm0,
+                                                 double* __restrict__ gm1, double* __restrict__ resid,
+                                                 const uint8_t* __restrict__ mark, int64_t U) {
   constexpr int H = K / 2, LZ = K + 4, LD2 = H + 4;
   __shared__ double Z1[16 * LZ];
   __shared__ double D2[16 * LD2];
@@ -204,6 +230,9 @@ __global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __res
     const bool v = my < N;
     const int32_t u_l = v ? self0[my] : 0, i_l = v ? other0[my] : 0, j_l = v ? row0[my] : 0;
     const float y_l = v ? rat0[my] : 0.f;
+    // fia_prepare_for: g_mlp of a side is needed only for rows in a cached entity's list
+    const bool need_u = v && (!mark || mark[u_l]), need_i = v && (!mark || mark[U + i_l]);
+    const bool any_u = __any(need_u), any_i = __any(need_i);
     __syncthreads();
     for (int r = 0; r < 16; ++r) {
       const int32_t u = __shfl(u_l, r), i = __shfl(i_l, r);
@@ -237,10 +266,28 @@ __global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __res
         acc = mfma4(D2[ml * LD2 + kk + kl], (double)W2[(16 * t + ml) * H + kk + kl], acc);
       const int c = 16 * t + ml;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = kl + 4 * r;
-        const int32_t j = __shfl(j_l, row);
-        if (p0 + row < N) d1s[(int64_t)j * K + c] = Z1[row * LZ + c] > 0.0 ? acc[r] : 0.0;
+      for (int r = 0; r < 4; ++r) {           // Z1 becomes D1 (each lane rewrites what it read)
+        double* z = Z1 + (kl + 4 * r) * LZ + c;
+        *z = *z > 0.0 ? acc[r] : 0.0;
+      }
+    }
+    __syncthreads();
+    // g_mlp of both sides: D1 . W1_side^T (W1 rows [0, k) act on Pm, rows [k, 2k) on Qm)
+#pragma unroll 1
+    for (int sd = 0; sd < 2; ++sd) {
+      if (!(sd ? any_i : any_u)) continue;
+      double* __restrict__ gm = sd ? gm1 : gm0;
+      for (int t = 0; t < K / 16; ++t) {
+        d4_t acc = {0.0, 0.0, 0.0, 0.0};
+        const float* __restrict__ wrow = W1 + (int64_t)(sd * K + 16 * t + ml) * K;
+#pragma unroll 4
+        for (int kk = 0; kk < K; kk += 4) acc = mfma4(Z1[ml * LZ + kk + kl], (double)wrow[kk + kl], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = kl + 4 * r;
+          const int32_t j = __shfl(j_l, row);
+          if (p0 + row < N) gm[(int64_t)j * K + 16 * t + ml] = acc[r];
+        }
       }
     }
     // r-hat per row: the MLP part sits in the 16 lanes of group (row & 3), register row >> 2
@@ -288,7 +335,6 @@ struct GramCfg {
   static constexpr int TPG = (NTL + NG - 1) / NG;
   static constexpr int PER = (TPG + kGW - 1) / kGW;
   static constexpr int LDG = M::NPs + 16;   // staged g row stride (doubles)
-  static constexpr int LDD = M::K + 4;      // staged d1 row stride
 };
 
 template <class M>
@@ -297,14 +343,12 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
                                                        const int32_t* __restrict__ other,
                                                        const int32_t* __restrict__ rowid,
                                                        const float* __restrict__ emb_other,
-                                                       const double* __restrict__ d1s, const float* __restrict__ W1,
-                                                       const float* __restrict__ W3, double* __restrict__ gram,
-                                                       double* __restrict__ part) {
+                                                       const double* __restrict__ gms, const float* __restrict__ W3,
+                                                       double* __restrict__ gram, double* __restrict__ part) {
   using C = GramCfg<M>;
-  constexpr int K = M::K, T = M::T, LDG = C::LDG, LDD = C::LDD, PER = C::PER;
+  constexpr int K = M::K, T = M::T, LDG = C::LDG, PER = C::PER;
   constexpr int64_t GW = gram_words<M>();
   __shared__ double Gs[16 * LDG];
-  __shared__ double Ds_[M::ncf ? 16 * LDD : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ml = lane & 15, kl = lane >> 4;
   const int grp = blockIdx.y;
@@ -321,7 +365,7 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
     tc_[p] = on_[p] ? idx - tr * (tr + 1) / 2 : 0;
   }
   for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
-    const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], slot = items[4 * it + 3];
+    const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], dst = items[4 * it + 3];
     const int64_t lb = ptr[e] + start;
     d4_t acc[PER];
 #pragma unroll
@@ -348,28 +392,16 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
         } else {
           constexpr int PERT = K / 32;
           const int32_t j = valid ? rowid[lb + t0 + r] : 0;
-          const double* dsrc = d1s + (int64_t)j * K + pp * PERT;
+          const double* msrc = gms + (int64_t)j * K + pp * PERT;
           const float* gsrc = emb_other + (int64_t)o * K + pp * PERT;
 #pragma unroll
           for (int c = 0; c < PERT; ++c) {
-            Ds_[r * LDD + pp * PERT + c] = valid ? dsrc[c] : 0.0;
+            Gs[r * LDG + pp * PERT + c] = valid ? msrc[c] : 0.0;
             Gs[r * LDG + K + pp * PERT + c] = valid ? (double)W3[M::H + pp * PERT + c] * (double)gsrc[c] : 0.0;
           }
         }
       }
       __syncthreads();
-      if constexpr (M::ncf) {
-        // g_mlp = D1 . W1_side^T  (16 ratings x k), output tiles over the waves
-        for (int at = wave; at < K / 16; at += kGW) {
-          d4_t a4 = {0.0, 0.0, 0.0, 0.0};
-          const float* wrow = W1 + (int64_t)(sd * K + 16 * at + ml) * K;
-#pragma unroll 4
-          for (int kk = 0; kk < K; kk += 4) a4 = mfma4(Ds_[ml * LDD + kk + kl], (double)wrow[kk + kl], a4);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Gs[(kl + 4 * r) * LDG + 16 * at + ml] = a4[r];
-        }
-        __syncthreads();
-      }
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const double* gr = Gs + (4 * s4 + kl) * LDG + ml;
@@ -378,7 +410,7 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
           if (on_[p]) acc[p] = mfma4(gr[16 * tr_[p]], gr[16 * tc_[p]], acc[p]);
       }
     }
-    double* out = slot < 0 ? gram + (int64_t)e * GW : part + (int64_t)slot * GW;
+    double* out = dst >= 0 ? gram + (int64_t)dst * GW : part + (int64_t)(-dst - 1) * GW;
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
       if (!on_[p]) continue;
@@ -392,11 +424,11 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
 __global__ void k_big_combine(int64_t n_comb, const int32_t* __restrict__ comb, int64_t GW,
                               const double* __restrict__ part, double* __restrict__ gram) {
   for (int64_t w = blockIdx.x; w < n_comb; w += gridDim.x) {
-    const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
+    const int32_t gs = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
     for (int64_t t = threadIdx.x; t < GW; t += blockDim.x) {
       double s = 0.0;
       for (int k = 0; k < ns; ++k) s += part[(int64_t)(first + k) * GW + t];
-      gram[(int64_t)e * GW + t] = s;
+      gram[(int64_t)gs * GW + t] = s;
     }
   }
 }
@@ -416,7 +448,8 @@ __global__ __launch_bounds__(256) void k_big_prologue(BigArgs A, int64_t Q, doub
   for (int64_t q = blockIdx.x; q < Q; q += gridDim.x) {
     const int32_t u = A.qu[q], i = A.qi[q];
     double* qw = qwork + q * M::QW;
-    const bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
+    bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
+    if (ok && A.slot[0]) ok = A.slot[0][u] >= 0 && A.slot[1][i] >= 0;   // not cached: NaN (checked by the ABI)
     const int64_t n = ok ? (A.ptr[0][u + 1] - A.ptr[0][u]) + (A.ptr[1][i + 1] - A.ptr[1][i]) : 0;
     if (n == 0) {
       if (tid == 0) qw[0] = 0.0;
@@ -507,33 +540,69 @@ __global__ __launch_bounds__(256) void k_big_prologue(BigArgs A, int64_t Q, doub
 }
 
 // ------------------------------------------------------------------------------------
-// Blocked left-looking LDL^T + solve, one 256-thread workgroup per system (persistent
+// Blocked left-looking LDL^T + solve, one 512-thread workgroup per system (persistent
 // over the list).  System = one side block (CPL = false, NP = NPs) or a full coupled
 // query (CPL = true, NP = 2 NPs).  Augmented matrix rows: [0, NP) the Hessian, NP the
 // right-hand side v^T, NP+1..NP+15 zero, so row NP of L is y = D^-1 L^-1 v.
-// L (column-major, LDR = NP + 16 rows) lives in this workgroup's scratch slab; panel
-// (NB columns x all rows below) in LDS.
+// L (column-major, LDR = NP + 16 rows) lives in this workgroup's scratch slab.  Per
+// panel of NB columns:
+//   (a) MFMA update of the panel rows from the factored columns (L streamed, D L^T of
+//       the panel rows on the fly), result in LDS;
+//   (b) one wave factors the NB x NB diagonal block in registers (readlane broadcasts);
+//   (c) every row below solves against it in registers (barrier-free TRSM) and writes
+//       its L row segment.
+// Then L^T x = y in 32-column blocks from the end: a one-wave triangle per block and a
+// GEMV update of the earlier entries, whose L operands are loaded behind the triangle.
 // ------------------------------------------------------------------------------------
-constexpr int kSolveMG = 4;   // row tiles per wave per MFMA pass
+constexpr int kSolveMG = 2;     // row tiles per wave per MFMA pass
+constexpr int PD = 8;           // k-steps in flight in the panel update
+// solve workgroup (8 waves: 2 per SIMD, 256 VGPRs each -- the 32-wide register rows of
+// the diagonal block / TRSM and the prefetch ring fit without spills)
+template <int NP>
+constexpr int solve_threads() { return 512; }
 
 template <int NP>
-constexpr int solve_nb() {
-  return ((NP + 16) * 33 + NP + 64) * 8 <= 160 * 1024 ? 32 : 16;
+constexpr int solve_nb() {   // 32-column panels when NP allows and LDS fits, else 16
+  return NP % 32 == 0 && ((NP + 16) * 33 + NP + 32 * 32 + 64) * 8 <= 160 * 1024 ? 32 : 16;
 }
 template <int NP>
 constexpr size_t solve_lds() {
-  return (size_t)((NP + 16) * (solve_nb<NP>() + 1) + NP + 64) * 8;
+  return (size_t)((NP + 16) * (solve_nb<NP>() + 1) + NP + solve_nb<NP>() * solve_nb<NP>() + 64) * 8;
+}
+
+__device__ __forceinline__ double readlane_dbl(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int NW>
+__device__ __forceinline__ double bsum(double x, double* red) {
+  x = wsum(x);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) t += red[w];
+  return t;
 }
 
 template <class M, int NP, bool CPL>
-__global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __restrict__ list,
+__global__ __launch_bounds__(solve_threads<NP>()) void k_big_solve(BigArgs A, const int32_t* __restrict__ list,
                                                    const double* __restrict__ qwork, double* __restrict__ lscr,
                                                    double* __restrict__ xb, double* __restrict__ rec) {
   constexpr int K = M::K, NPs = M::NPs, Ds = M::Ds, NB = solve_nb<NP>(), LDR = NP + 16, LDP = NB + 1;
   constexpr int NRT = LDR / 16, NCT = NB / 16, MG = kSolveMG;
   constexpr int64_t GW = gram_words<M>();
+  constexpr int kST = solve_threads<NP>(), kSW = kST / 64;
+  constexpr int CPT = (NP + kST - 1) / kST;    // backward-solve columns per thread
+  constexpr int BW = CPT == 1 && NB == 32 ? 32 : 16;   // backward-solve block (<= NB: staged in W11)
+  static_assert(BW <= NB, "backward blocks are staged in W11");
   __shared__ double P[LDR * LDP];
   __shared__ double dd[NP];
+  __shared__ double W11[NB * NB];              // W11[j][jj] = L[c0+j][c0+jj] d[c0+jj], jj < j
   __shared__ double red[64];
   double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * LDR * NP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -547,8 +616,8 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
     const double s2n = 2.0 / qw[0], cdup = qw[1], esum = qw[2];
     const double* __restrict__ vv = qw + 8 + (CPL ? 0 : sd * NPs);   // v of this system
     const int32_t u = A.qu[q], i = A.qi[q];
-    const double* __restrict__ G0 = A.gram[0] + (int64_t)u * GW;
-    const double* __restrict__ G1 = A.gram[1] + (int64_t)i * GW;
+    const double* __restrict__ G0 = A.gram[0] + (int64_t)(A.slot[0] ? A.slot[0][u] : u) * GW;
+    const double* __restrict__ G1 = A.gram[1] + (int64_t)(A.slot[1] ? A.slot[1][i] : i) * GW;
     auto aorig = [&](int r, int c) -> double {
       if (r >= NP) return (r == NP && c < NP) ? vv[c] : 0.0;
       if constexpr (!CPL) {
@@ -582,7 +651,7 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
       const int rt0 = c0 >> 4, nrt = NRT - rt0;
       const int nbe = NP - c0 < NB ? NP - c0 : NB;   // last panel of NP = 16 (2m+1): one tile column
       // (a) panel rows [c0, LDR) x cols [c0, c0 + NB): A - L[:, :c0] D L[c0:c0+NB, :c0]^T
-      for (int gb = wave * MG; gb < nrt; gb += 4 * MG) {
+      for (int gb = wave * MG; gb < nrt; gb += kSW * MG) {
         d4_t acc[MG][NCT];
 #pragma unroll
         for (int m = 0; m < MG; ++m)
@@ -591,21 +660,34 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               acc[m][ct][r] = gb + m < nrt ? aorig(16 * (rt0 + gb + m) + kl + 4 * r, c0 + 16 * ct + ml) : 0.0;
-#pragma unroll 2
-        for (int kk = 0; kk < c0; kk += 4) {
-          const int kc = kk + kl;
+        // k-steps (4 factored columns each) stream through a ring of PD register slots:
+        // step s + PD is loaded while step s is multiplied (L comes from MALL/HBM)
+        const int nst = c0 >> 2;
+        double ra[PD][MG], rb[PD][NCT];
+        auto ld = [&](int st, double (&a)[MG], double (&b)[NCT]) {
+          const int kc = 4 * st + kl;
           const double* __restrict__ Lc = Ls + (int64_t)kc * LDR;
           const double dk = dd[kc];
-          double b[NCT], a[MG];
 #pragma unroll
           for (int ct = 0; ct < NCT; ++ct) b[ct] = Lc[c0 + 16 * ct + ml] * dk;
 #pragma unroll
           for (int m = 0; m < MG; ++m) a[m] = gb + m < nrt ? -Lc[16 * (rt0 + gb + m) + ml] : 0.0;
+        };
 #pragma unroll
-          for (int m = 0; m < MG; ++m)
-            if (gb + m < nrt)
+        for (int d = 0; d < PD; ++d)
+          if (d < nst) ld(d, ra[d], rb[d]);
+        for (int s0 = 0; s0 < nst; s0 += PD) {
 #pragma unroll
-              for (int ct = 0; ct < NCT; ++ct) acc[m][ct] = mfma4(a[m], b[ct], acc[m][ct]);
+          for (int d = 0; d < PD; ++d) {
+            if (s0 + d < nst) {
+#pragma unroll
+              for (int m = 0; m < MG; ++m)
+                if (gb + m < nrt)
+#pragma unroll
+                  for (int ct = 0; ct < NCT; ++ct) acc[m][ct] = mfma4(ra[d][m], rb[d][ct], acc[m][ct]);
+              if (s0 + d + PD < nst) ld(s0 + d + PD, ra[d], rb[d]);
+            }
+          }
         }
 #pragma unroll
         for (int m = 0; m < MG; ++m)
@@ -616,48 +698,96 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
               for (int r = 0; r < 4; ++r) P[(16 * (gb + m) + kl + 4 * r) * LDP + 16 * ct + ml] = acc[m][ct][r];
       }
       __syncthreads();
-      // (b) factor the panel in LDS, one thread per row (right-looking inside the panel)
-      const int prow = LDR - c0;
-      for (int j = 0; j < nbe; ++j) {
-        const double dc = P[j * LDP + j];
-        for (int rr = j + 1 + tid; rr < prow; rr += 256) {
-          double* __restrict__ Pr = P + rr * LDP;
-          const double f = Pr[j] / dc;
-          const int jm = rr + 1 < nbe ? rr + 1 : nbe;
-          for (int jj = j + 1; jj < jm; ++jj) Pr[jj] = fma(-f, P[jj * LDP + j], Pr[jj]);
+      // (b) diagonal block: lane r owns row r; right-looking LDL^T with readlane broadcasts
+      if (wave == 0) {
+        double a[NB];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) a[t] = lane < nbe ? P[lane * LDP + t] : (lane == t ? 1.0 : 0.0);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          // entries right of a lane's diagonal become garbage and are never read
+          const double dj = readlane_dbl(a[j], j);
+          const double f = lane > j ? a[j] / dj : 0.0;   // lane r > j: L[r][j]
+#pragma unroll
+          for (int t = j + 1; t < NB; ++t) a[t] = fma(-f, readlane_dbl(a[j], t), a[t]);
         }
-        __syncthreads();
+        double dl = a[0];
+#pragma unroll
+        for (int t = 1; t < NB; ++t) dl = t == lane ? a[t] : dl;   // static indices only (no scratch)
+        if (lane < nbe) {
+          double* __restrict__ Wr = W11 + lane * NB;
+#pragma unroll
+          for (int t = 0; t < NB; ++t)
+            if (t < lane) Wr[t] = a[t];
+          dd[c0 + lane] = dl;
+        }
+        // L of the block (rows c0 + r > c0 + t): a[t] / d_t
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const double dt = readlane_dbl(dl, t);
+          if (lane < nbe && t < lane) Ls[(int64_t)(c0 + t) * LDR + c0 + lane] = a[t] / dt;
+        }
       }
-      if (tid < nbe) dd[c0 + tid] = P[tid * LDP + tid];
       __syncthreads();
-      // (c) L columns of the panel (rows below the diagonal, v row included)
-      for (int j = 0; j < nbe; ++j) {
-        const int c = c0 + j;
-        const double inv = 1.0 / dd[c];
-        double* __restrict__ Lc = Ls + (int64_t)c * LDR;
-        for (int r = c + 1 + tid; r < LDR; r += 256) Lc[r] = P[(r - c0) * LDP + j] * inv;
+      // (c) rows below the block: u_j = A[r][j] - sum_{jj<j} L[r][jj] W11[j][jj],  L[r][j] = u_j / d_j
+      for (int r = c0 + nbe + tid; r < LDR; r += kST) {
+        double p[NB];
+        const double* __restrict__ Pr = P + (r - c0) * LDP;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) p[t] = Pr[t];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          double s = p[j];
+          const double* __restrict__ Wj = W11 + j * NB;
+#pragma unroll
+          for (int jj = 0; jj < j; ++jj) s = fma(-p[jj], Wj[jj], s);
+          p[j] = j < nbe ? s / dd[c0 + (j < nbe ? j : 0)] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+          if (j < nbe) Ls[(int64_t)(c0 + j) * LDR + r] = p[j];
       }
       __syncthreads();
     }
-    // backward solve L^T x = y, y_c = L[NP][c]; 16-column blocks from the end
+    // backward solve L^T x = y, y_c = L[NP][c]; BW-column blocks from the end.  Per block
+    // one global round trip: the GEMV operands of the earlier columns and the block's
+    // triangle (staged into W11) are loaded together, then the triangle (one wave, LDS)
+    // and the GEMV update.
     double* __restrict__ xs = P;
-    for (int bt = NP / 16 - 1; bt >= 0; --bt) {
-      const int cb = 16 * bt;
-      for (int cc = wave; cc < 16; cc += 4) {
-        const double* __restrict__ Lc = Ls + (int64_t)(cb + cc) * LDR;
-        double acc = 0.0;
-        for (int r = cb + 16 + lane; r < NP; r += 64) acc = fma(Lc[r], xs[r], acc);
-        acc = wsum(acc);
-        if (lane == 0) red[cc] = acc;
+    for (int c = tid; c < NP; c += kST) xs[c] = Ls[(int64_t)c * LDR + NP];
+    for (int b0 = ((NP - 1) / BW) * BW; b0 >= 0; b0 -= BW) {
+      const int bw = NP - b0 < BW ? NP - b0 : BW;
+      double lv[CPT][BW];
+#pragma unroll
+      for (int cc = 0; cc < CPT; ++cc) {
+        const int c = tid + cc * kST;
+#pragma unroll
+        for (int t = 0; t < BW; ++t) lv[cc][t] = (c < b0 && t < bw) ? Ls[(int64_t)c * LDR + b0 + t] : 0.0;
+      }
+      for (int e = tid; e < BW * BW; e += kST) {     // W11[c][t] = L[b0 + t][b0 + c], t > c
+        const int cc = e / BW, t = e - cc * BW;
+        W11[e] = (cc < bw && t < bw && t > cc) ? Ls[(int64_t)(b0 + cc) * LDR + b0 + t] : 0.0;
       }
       __syncthreads();
       if (wave == 0) {
-        double val = lane < 16 ? Ls[(int64_t)(cb + lane) * LDR + NP] - red[lane] : 0.0;
-        for (int rl = 15; rl >= 0; --rl) {
-          const double xr = __shfl(val, rl);
-          if (lane < rl) val = fma(-Ls[(int64_t)(cb + lane) * LDR + cb + rl], xr, val);
+        double val = lane < bw ? xs[b0 + lane] : 0.0;
+        const double* __restrict__ Wc = W11 + (lane < BW ? lane : 0) * BW;
+        for (int t = bw - 1; t >= 0; --t) {
+          const double xt = readlane_dbl(val, t);
+          if (lane < t) val = fma(-Wc[t], xt, val);
         }
-        if (lane < 16) xs[cb + lane] = val;
+        if (lane < bw) xs[b0 + lane] = val;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int cc = 0; cc < CPT; ++cc) {
+        const int c = tid + cc * kST;
+        if (c < b0) {
+          double s = xs[c];
+#pragma unroll
+          for (int t = 0; t < BW; ++t) s = fma(-lv[cc][t], xs[b0 + t], s);
+          xs[c] = s;
+        }
       }
       __syncthreads();
     }
@@ -670,7 +800,7 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
       const double* __restrict__ th = qw + 8 + 2 * NPs + side * NPs;
       double* __restrict__ xo = xb + q * 2 * NPs + side * NPs;
       double cq = 0.0, xv = 0.0;
-      for (int a = tid; a < NPs; a += 256) {
+      for (int a = tid; a < NPs; a += kST) {
         const double xa = xsd[a];
         xo[a] = xa;
         if (a < Ds) {
@@ -678,22 +808,19 @@ __global__ __launch_bounds__(256) void k_big_solve(BigArgs A, const int32_t* __r
           xv = fma(xa, vsd[a], xv);
         }
       }
-      cq = bsum256(cq, red);
-      xv = bsum256(xv, red);
+      cq = bsum<kSW>(cq, red);
+      xv = bsum<kSW>(xv, red);
       double* __restrict__ S = R + 8 + side * M::SB;
       if (tid == 0) {
         R[4 + 2 * side] = A.wd * cq;
         R[5 + 2 * side] = xv;
       }
       if constexpr (!M::ncf) {
-        for (int a = tid; a <= K; a += 256) S[a] = xsd[a];
+        for (int a = tid; a <= K; a += kST) S[a] = xsd[a];
         if (tid == 0) S[K + 1] = (double)(side ? u : i);
       } else {
-        const float* __restrict__ W1 = A.t[4];
-        for (int c = tid; c < K; c += 256) {
-          double y = 0.0;
-          for (int a = 0; a < K; ++a) y = fma(xsd[a], (double)W1[(int64_t)(side * K + a) * K + c], y);
-          S[c] = y;
+        for (int c = tid; c < K; c += kST) {
+          S[c] = xsd[c];
           S[K + c] = (double)A.t[8][M::H + c] * xsd[K + c];
         }
         if (tid == 0) S[2 * K] = (double)(side ? u : i);
@@ -732,7 +859,7 @@ __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __re
 // Entity-shared scoring (work items from build_groups: one <= kChunk chunk of one
 // entity's list x one block of <= kQueryBlock queries with that entity).  Per rating:
 //   MF  s_q = x_emb,q . emb_other + x_bias,q
-//   NCF s_q = (W1_s^T x_mlp,q) . d1_j + (W3g * x_gmf,q) . gmf_other
+//   NCF s_q = x_mlp,q . g_mlp,j + (W3g * x_gmf,q) . gmf_other
 //   influence = (2 e_j s_q + c_q) / n_q   (mf:240-246); the test pair's own train row
 //   takes e and s = x.v from the record (bit-identical copies).
 // ------------------------------------------------------------------------------------
@@ -813,7 +940,7 @@ __global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
         }
       }
       if constexpr (M::ncf) {
-        const double2* __restrict__ dsrc = reinterpret_cast<const double2*>(A.d1 + (int64_t)row * K);
+        const double2* __restrict__ dsrc = reinterpret_cast<const double2*>(A.gm[sd] + (int64_t)row * K);
 #pragma unroll 2
         for (int c2 = 0; c2 < K / 2; c2 += 2) {
           const double2 a0 = dsrc[c2], a1 = dsrc[c2 + 1];
@@ -891,9 +1018,10 @@ BigArgs make_big_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
     A.rating[s] = c->idx.side[s].rating.as<float>();
     A.gram[s] = c->gram[s].as<double>();
     A.l1[s] = c->l1[s].as<double>();
+    A.gm[s] = c->gm[s].as<double>();
+    A.slot[s] = c->subset ? c->slot[s].as<int32_t>() : nullptr;
   }
   A.resid = c->resid.as<double>();
-  A.d1 = c->d1.as<double>();
   for (int t = 0; t < 10; ++t) A.t[t] = c->p.t[t];
   A.wd = c->p.wd;
   A.damping = c->p.damping;
@@ -918,53 +1046,96 @@ int cu_count(fia_ctx* c) {
   return c->num_cus;
 }
 
-// Gram work lists for the current index: slices of <= kBigSlice ratings, longest lists
-// first; split lists get partial slots summed by k_big_combine in slot order.
-hipError_t big_work_lists(fia_ctx* c) {
+// Gram work lists: slices of <= kBigSlice ratings of every cached entity, longest lists
+// first; items {entity, start, len, dst} with dst >= 0 the cache slot, dst < 0 the partial
+// slot -dst-1 of a split list; split lists get a combine entry {cache slot, first partial,
+// n partials, 0} summed in slot order.  marks == nullptr: every entity, slot = entity id
+// (lists cached per index); else only the marked entities, numbered in entity order.
+hipError_t big_work_lists(fia_ctx* c, const std::vector<uint8_t>* marks) {
   Index& X = c->idx;
-  if (c->bitems_version == X.version) return hipSuccess;
+  if (!marks && !c->subset && c->bitems_version == X.version) return hipSuccess;
+  if (c->border_version != X.version) {
+    for (int sd = 0; sd < 2; ++sd) {
+      const std::vector<int64_t>& hp = X.hptr[sd];
+      const int64_t ne = (int64_t)hp.size() - 1;
+      std::vector<int32_t>& ord = c->border[sd];
+      ord.resize((size_t)ne);
+      for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = (int32_t)e;
+      std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+        return hp[(size_t)a + 1] - hp[(size_t)a] > hp[(size_t)b + 1] - hp[(size_t)b];
+      });
+    }
+    c->border_version = X.version;
+  }
   for (int sd = 0; sd < 2; ++sd) {
     const std::vector<int64_t>& hp = X.hptr[sd];
     const int64_t ne = (int64_t)hp.size() - 1;
-    std::vector<int32_t> ord((size_t)ne);
-    for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = (int32_t)e;
-    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
-      return hp[(size_t)a + 1] - hp[(size_t)a] > hp[(size_t)b + 1] - hp[(size_t)b];
-    });
+    std::vector<int32_t> slot((size_t)ne, -1);
+    int32_t ncache = 0;
+    for (int64_t e = 0; e < ne; ++e)
+      if (!marks || marks[sd][(size_t)e]) slot[(size_t)e] = ncache++;
     std::vector<int32_t> items, comb;
-    int32_t slots = 0;
-    for (int32_t e : ord) {
+    int32_t parts = 0;
+    for (int32_t e : c->border[sd]) {
+      if (slot[(size_t)e] < 0) continue;
       const int64_t len = hp[(size_t)e + 1] - hp[(size_t)e];
       const int64_t nit = len == 0 ? 1 : (len + kBigSlice - 1) / kBigSlice;
-      if (nit > 1) comb.insert(comb.end(), {e, slots, (int32_t)nit, 0});
+      if (nit > 1) comb.insert(comb.end(), {slot[(size_t)e], parts, (int32_t)nit, 0});
       for (int64_t t = 0; t < nit; ++t) {
         const int64_t st = t * kBigSlice;
         const int64_t ln = std::min<int64_t>(kBigSlice, len - st);
-        items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), nit > 1 ? slots++ : -1});
+        const int32_t dst = nit > 1 ? -(1 + parts++) : slot[(size_t)e];
+        items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), dst});
       }
     }
     c->n_bitems[sd] = (int64_t)items.size() / 4;
     c->n_bcomb[sd] = (int64_t)comb.size() / 4;
-    c->n_bslots[sd] = slots;
-    FIA_HIP_TRY(c->bitems[sd].reserve(sizeof(int32_t) * items.size()));
-    FIA_HIP_TRY(hipMemcpy(c->bitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+    c->n_bslots[sd] = parts;
+    c->n_bcache[sd] = ncache;
+    if (!items.empty()) {
+      FIA_HIP_TRY(c->bitems[sd].reserve(sizeof(int32_t) * items.size()));
+      FIA_HIP_TRY(hipMemcpy(c->bitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+    }
     if (!comb.empty()) {
       FIA_HIP_TRY(c->bcomb[sd].reserve(sizeof(int32_t) * comb.size()));
       FIA_HIP_TRY(hipMemcpy(c->bcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
     }
+    if (marks) {
+      FIA_HIP_TRY(c->slot[sd].reserve(sizeof(int32_t) * (size_t)(ne + 1)));
+      FIA_HIP_TRY(hipMemcpy(c->slot[sd].ptr, slot.data(), sizeof(int32_t) * slot.size(), hipMemcpyHostToDevice));
+    }
   }
-  c->bitems_version = X.version;
+  c->bitems_version = marks ? ~0ull : X.version;
+  c->subset = marks != nullptr;
   return hipSuccess;
 }
 
 template <class M>
-hipError_t prepare_big_impl(fia_ctx* c, hipStream_t s) {
+hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s) {
   constexpr int K = M::K;
   constexpr int64_t GW = gram_words<M>();
   Index& X = c->idx;
   const int64_t N = X.N;
   const int64_t n_ent[2] = {c->p.U, c->p.I};
   const unsigned gN = grid_cap((N + 255) / 256, 16384);
+  // entity selection first (host round trip), so a too-large cache fails before any work
+  std::vector<uint8_t> marks[2];
+  if (qu) {
+    FIA_HIP_TRY(c->mark.reserve((size_t)(n_ent[0] + n_ent[1])));
+    FIA_HIP_TRY(hipMemsetAsync(c->mark.ptr, 0, (size_t)(n_ent[0] + n_ent[1]), s));
+    if (Q > 0) {
+      hipLaunchKernelGGL(k_mark, dim3(grid_cap((Q + 255) / 256, 4096)), dim3(256), 0, s, Q, qu, qi, n_ent[0],
+                         n_ent[1], c->mark.as<uint8_t>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+    marks[0].resize((size_t)n_ent[0]);
+    marks[1].resize((size_t)n_ent[1]);
+    FIA_HIP_TRY(hipMemcpyAsync(marks[0].data(), c->mark.ptr, (size_t)n_ent[0], hipMemcpyDeviceToHost, s));
+    FIA_HIP_TRY(hipMemcpyAsync(marks[1].data(), c->mark.as<uint8_t>() + n_ent[0], (size_t)n_ent[1],
+                               hipMemcpyDeviceToHost, s));
+    FIA_HIP_TRY(hipStreamSynchronize(s));
+  }
+  FIA_HIP_TRY(big_work_lists(c, qu ? marks : nullptr));
   if (c->self_version != X.version) {
     for (int sd = 0; sd < 2; ++sd) {
       FIA_HIP_TRY(c->self[sd].reserve(sizeof(int32_t) * (size_t)(N + 1)));
@@ -990,28 +1161,27 @@ hipError_t prepare_big_impl(fia_ctx* c, hipStream_t s) {
       hipLaunchKernelGGL(k_l1_big<K>, dim3(grid_cap((n_ent[sd] * K + 255) / 256, 16384)), dim3(256), 0, s,
                          c->p.t[sd], c->p.t[4], sd * K, n_ent[sd], c->l1[sd].as<double>());
       FIA_HIP_TRY(hipGetLastError());
+      FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1)));
     }
-    FIA_HIP_TRY(c->d1.reserve(sizeof(double) * (size_t)(N * K + 1)));
     if (N > 0) {
       hipLaunchKernelGGL(k_ncf_rows<K>, dim3(grid_cap((N + 15) / 16, 65536)), dim3(64), 0, s, N,
                          c->self[0].as<int32_t>(), X.side[0].other.as<int32_t>(), X.side[0].row.as<int32_t>(),
                          X.side[0].rating.as<float>(), c->l1[0].as<double>(), c->l1[1].as<double>(), c->p.t[5],
-                         c->p.t[6], c->p.t[7], c->p.t[8], c->p.t[9], c->p.t[2], c->p.t[3], c->d1.as<double>(),
-                         c->resid.as<double>());
+                         c->p.t[6], c->p.t[7], c->p.t[8], c->p.t[9], c->p.t[2], c->p.t[3], c->p.t[4],
+                         c->gm[0].as<double>(), c->gm[1].as<double>(), c->resid.as<double>(),
+                         qu ? c->mark.as<uint8_t>() : (const uint8_t*)nullptr, n_ent[0]);
       FIA_HIP_TRY(hipGetLastError());
     }
   }
-  FIA_HIP_TRY(big_work_lists(c));
   for (int sd = 0; sd < 2; ++sd) {
-    FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * GW)));
+    FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)((c->n_bcache[sd] > 0 ? c->n_bcache[sd] : 1) * GW)));
     if (c->n_bslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(c->n_bslots[sd] * GW)));
     const float* emb_other = M::ncf ? c->p.t[sd == 0 ? 3 : 2] : c->p.t[sd == 0 ? 1 : 0];
     if (c->n_bitems[sd] > 0) {
       hipLaunchKernelGGL(k_big_gram<M>, dim3(grid_cap(c->n_bitems[sd], 1 << 20), GramCfg<M>::NG), dim3(64 * kGW), 0, s,
                          sd, c->n_bitems[sd], c->bitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(),
                          X.side[sd].other.as<int32_t>(), X.side[sd].row.as<int32_t>(), emb_other,
-                         c->d1.as<double>(), c->p.t[4], c->p.t[8], c->gram[sd].as<double>(),
-                         c->gpart[sd].as<double>());
+                         c->gm[sd].as<double>(), c->p.t[8], c->gram[sd].as<double>(), c->gpart[sd].as<double>());
       FIA_HIP_TRY(hipGetLastError());
     }
     if (c->n_bcomb[sd] > 0) {
@@ -1032,7 +1202,7 @@ hipError_t launch_solve(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int
   const int64_t grid = max_sys < resident ? max_sys : resident;
   constexpr int64_t slab = (int64_t)(NP + 16) * NP;
   FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(grid * slab)));
-  hipLaunchKernelGGL((k_big_solve<M, NP, CPL>), dim3((unsigned)grid), dim3(256), 0, s, A, list,
+  hipLaunchKernelGGL((k_big_solve<M, NP, CPL>), dim3((unsigned)grid), dim3(solve_threads<NP>()), 0, s, A, list,
                      c->qwork.as<double>(), c->lscr.as<double>(), c->xb.as<double>(), c->rec.as<double>());
   return hipGetLastError();
 }
@@ -1096,11 +1266,18 @@ bool big_supported(int model, int k) {
   return false;
 }
 
-hipError_t prepare_big(fia_ctx* c, hipStream_t s) {
-#define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_big_impl<T>(c, s);
+hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s) {
+#define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_big_impl<T>(c, Q, qu, qi, s);
   FIA_BIG_CASES(X)
 #undef X
   return hipErrorInvalidValue;
+}
+
+hipError_t check_cover(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag, hipStream_t s) {
+  if (!c->subset || Q <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_check_cover, dim3(grid_cap((Q + 255) / 256, 4096)), dim3(256), 0, s, Q, qu, qi, c->p.U,
+                     c->p.I, c->slot[0].as<int32_t>(), c->slot[1].as<int32_t>(), flag);
+  return hipGetLastError();
 }
 
 hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,

@@ -169,9 +169,14 @@ struct fia_ctx {
   fia::DevBuf self[2];    // int32 [N] entity owning list position p of side s
   uint64_t self_version = ~0ull;
   fia::DevBuf resid;      // double [N]   e_j = r-hat_j - y_j by train row
-  fia::DevBuf d1;         // double [N*k] NCF masked backward vector by train row
+  fia::DevBuf gm[2];      // double [N*k] NCF g_mlp = W1_side . d1_j by train row, per side
+  fia::DevBuf slot[2];    // int32 [n_entity] Gram cache slot (-1 = not cached) after fia_prepare_for
+  fia::DevBuf mark;       // uint8 [U + I] entities referenced by the fia_prepare_for queries
+  bool subset = false;    // caches cover only the fia_prepare_for entities (large-k models)
   fia::DevBuf bitems[2], bcomb[2];   // large-k Gram work lists {entity, start, len, slot}
-  int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0};
+  int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0}, n_bcache[2] = {0, 0};
+  std::vector<int32_t> border[2];   // entities by list length, longest first (host)
+  uint64_t border_version = ~0ull;
   uint64_t bitems_version = ~0ull;
   int bitems_k = 0;
   fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta
@@ -213,7 +218,10 @@ bool model_supported(int model, int k);
 
 // large-k models (bigk.hip): MF k in {128, 256}, NCF k in {64, 128, 256}
 bool big_supported(int model, int k);
-hipError_t prepare_big(fia_ctx* c, hipStream_t s);
+// qu == nullptr: caches for every entity; else only for the entities of the Q queries
+hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s);
+// flag[2] |= 1 if a query's user or item has no cache after fia_prepare_for
+hipError_t check_cover(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag, hipStream_t s);
 hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                      int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);

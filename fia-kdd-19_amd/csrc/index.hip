@@ -189,14 +189,21 @@ __global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __re
   }
 }
 
+// thread per work item (grid-stride up to wstart[nE]): its entity by binary search over
+// wstart, then {entity, chunk of the entity's list, block of the entity's query group}
 __global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned long long* __restrict__ gcnt,
                             int64_t nE, int32_t* __restrict__ witems) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nE) return;
-  const int64_t b = wstart[t], e = wstart[t + 1];
-  const int64_t nqb = ((int64_t)gcnt[t] + kQueryBlock - 1) / kQueryBlock;
-  for (int64_t w = b; w < e; ++w) {
-    witems[3 * w] = (int32_t)t;
+  const int64_t total = wstart[nE];
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nE - 1;     // last entity t with wstart[t] <= w
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (wstart[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const int64_t b = wstart[lo];
+    const int64_t nqb = ((int64_t)gcnt[lo] + kQueryBlock - 1) / kQueryBlock;
+    witems[3 * w] = (int32_t)lo;
     witems[3 * w + 1] = (int32_t)((w - b) / nqb);    // chunk of the entity's list
     witems[3 * w + 2] = (int32_t)((w - b) % nqb);    // block of the entity's query group
   }
@@ -417,7 +424,7 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                      c->gq.as<int32_t>(), c->wcnt.as<int64_t>());
   FIA_HIP_TRY(hipGetLastError());
   FIA_HIP_TRY(exclusive_scan_i64(c, c->wcnt.as<int64_t>(), c->wstart.as<int64_t>(), nE + 1, s));
-  hipLaunchKernelGGL(k_item_fill, dim3((unsigned)((nE + 255) / 256)), dim3(256), 0, s, c->wstart.as<int64_t>(),
+  hipLaunchKernelGGL(k_item_fill, dim3(grid_for(max_items, 256, 16384)), dim3(256), 0, s, c->wstart.as<int64_t>(),
                      c->gcnt.as<unsigned long long>(), nE, c->witems.as<int32_t>());
   return hipGetLastError();
 }

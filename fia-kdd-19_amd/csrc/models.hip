@@ -1769,7 +1769,7 @@ hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported) {
 #define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_impl<T>(c, s);
   FIA_MODEL_CASES(X)
 #undef X
-  if (big_supported(c->p.model, c->p.k)) return prepare_big(c, s);
+  if (big_supported(c->p.model, c->p.k)) return prepare_big(c, 0, nullptr, nullptr, s);
   unsupported = true;
   return hipSuccess;
 }

@@ -33,6 +33,7 @@ SIGNATURES = {
                                       ctypes.c_double, ctypes.c_double]),
     "fia_build_index": (ctypes.c_int, [_P, _I64, _I64, _I64, _P, _P, _P, _P]),
     "fia_prepare": (ctypes.c_int, [_P, _P]),
+    "fia_prepare_for": (ctypes.c_int, [_P, _I64, _P, _P, _P]),
     "fia_count_related": (ctypes.c_int, [_P, _I64, _P, _P, _P, ctypes.POINTER(_I64), _P]),
     "fia_related": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "fia_query_batch": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P]),
@@ -124,6 +125,10 @@ class Context(object):
 
     def prepare(self):
         self._check(self.lib.fia_prepare(self.h, _stream()), "fia_prepare")
+
+    def prepare_for(self, qu, qi):
+        """Hessian caches for only the users/items of these queries (large-k models)."""
+        self._check(self.lib.fia_prepare_for(self.h, qu.numel(), _ptr(qu), _ptr(qi), _stream()), "fia_prepare_for")
 
     def num_params(self):
         return self.lib.fia_num_params(self.h)

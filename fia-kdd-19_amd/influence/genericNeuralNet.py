@@ -81,6 +81,13 @@ class GenericNeuralNet(object):
         self._upload_params()
         self.ctx.prepare()
 
+    def prepare_for(self, test_indices):
+        """Rebuild the Hessian caches for only the users/items of these test ratings
+        (fia_prepare_for: one GPU's share of a sharded query set at large k).  Queries
+        outside the set then raise FIAError until the next prepare."""
+        qu, qi = self._query_tensors(test_indices)
+        self.ctx.prepare_for(qu, qi)
+
     def get_all_params(self):
         """Parameter values in the reference's get_all_params order (mf:30-36)."""
         return [self.params[n] for n in self.PARAM_NAMES]

@@ -302,3 +302,32 @@ def test_large_k_matches_oracle(model, k, tmp_path):
     rel, infl = res["rel_idx"][b:e], res["influence"][b:e]
     for row in np.unique(rel[np.bincount(rel)[rel] > 1]):
         assert (infl[rel == row] == infl[rel == row][0]).all()
+
+
+@pytest.mark.parametrize("model,k", [("MF", 128), ("NCF", 64)])
+def test_prepare_for_subset(model, k, tmp_path):
+    """fia_prepare_for: caches for only the queried users/items give the same
+    results as the full prepare, and a query outside the set is rejected."""
+    from influence._lib import FIAError
+    rng = np.random.default_rng(5)
+    U, I, N = 300, 40, 4000
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = synth.mf_params(U, I, k, 1) if model == "MF" else synth.ncf_params(U, I, k, 1)
+    qu = rng.integers(0, U, 12).astype(np.int32)
+    qi = rng.integers(0, I, 12).astype(np.int32)
+    qu[11], qi[11] = U - 1, I - 1
+    m = make_model(model, U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    full = m.get_influence_batch(list(range(12)), K=2)
+    subset = [q for q in range(11) if qu[q] != U - 1 and qi[q] != I - 1]
+    m.prepare_for(subset)
+    part = m.get_influence_batch(subset, K=2)
+    for j, q in enumerate(subset):
+        b, e = full["offsets"][q], full["offsets"][q + 1]
+        pb, pe = part["offsets"][j], part["offsets"][j + 1]
+        assert np.array_equal(part["rel_idx"][pb:pe], full["rel_idx"][b:e])
+        assert np.array_equal(part["influence"][pb:pe], full["influence"][b:e])   # same kernels, same bits
+        assert np.array_equal(part["x"][j], full["x"][q])
+    with pytest.raises(FIAError):
+        m.get_influence_batch([11], K=1)

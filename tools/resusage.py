@@ -29,5 +29,5 @@ for line in out.splitlines():
 for r in rows:
     if flt and flt not in r["name"]:
         continue
-    print("%-60s V%-4s A%-4s S%-3s VS%-3s LDS %-7s occ %s" % (r["name"][:60], r.get("VGPRs"), r.get("AGPRs"),
-          r.get("SGPRs"), r.get("VGPRs Spill"), r.get("LDS Size [bytes/block]"), r.get("Occupancy [waves/SIMD]")))
+    print("%-58s V%-4s A%-4s VS%-3s scr %-5s LDS %-7s occ %s" % (r["name"][:58], r.get("VGPRs"), r.get("AGPRs"),
+          r.get("VGPRs Spill"), r.get("ScratchSize [bytes/lane]"), r.get("LDS Size [bytes/block]"), r.get("Occupancy [waves/SIMD]")))
