@@ -185,7 +185,7 @@ struct fia_ctx {
   fia::DevBuf cpllist;    // int32 [1 + Q]  {count, q ...} coupled full systems
   fia::DevBuf lscr;       // double LDL^T factor scratch, one slab per resident solve workgroup
   int num_cus = 0;
-  bool score_grouped = false;   // scoring schedule, see fia_create
+  int score_mode = -1;    // scoring schedule: -1 auto, 0 per-query chunks, 1 entity-shared (FIA_SCORE)
   bool profiling = false;
   fia::PhaseEvents events;
 };

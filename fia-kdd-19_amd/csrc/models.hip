@@ -1669,7 +1669,11 @@ template <class M>
 hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                       int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
-  const bool grouped = c->score_grouped;
+  // Auto schedule (measured on MI355X, profiles/): entity-shared scoring wins whenever
+  // the per-rating work is larger than a 64-B gather (NCF's MLP, k >= 32) -- yelp-ex NCF
+  // 15.8 vs 13.3 M q/s, 20M MF k=64 855 vs 429 k q/s; for MF k <= 16 the group build
+  // costs more than the shared gathers save (ml-1m-ex 36.6 vs 39.3 M q/s).
+  const bool grouped = c->score_mode >= 0 ? c->score_mode == 1 : (M::ncf || M::K >= 32);
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   const int spc = grouped ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));

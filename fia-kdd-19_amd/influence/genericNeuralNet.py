@@ -7,6 +7,10 @@ Reference: src/influence/genericNeuralNet.py (GenericNeuralNet.__init__
 152-351 / NCF.py:43-66, 181-380.  Training (gnn:367-449), the classic
 full-parameter influence variants (gnn:511-808) and TF checkpoints are not
 part of this build.
+
+Training and leave-one-out retraining (gnn:344-412) run
+on influence/train.py (PyTorch-ROCm, TF-Adam); checkpoints are npz files with
+the parameters and the Adam state (the TF Saver keeps both, gnn:149, 410).
 """
 import os
 import time
@@ -92,18 +96,170 @@ class GenericNeuralNet(object):
         """Parameter values in the reference's get_all_params order (mf:30-36)."""
         return [self.params[n] for n in self.PARAM_NAMES]
 
+    @property
+    def checkpoint_file(self):
+        return os.path.join(self.train_dir, "%s-checkpoint" % self.model_name)   # gnn:169
+
     def save_checkpoint(self, step):
-        path = os.path.join(self.train_dir, "%s-checkpoint-%s.npz" % (self.model_name, step))
-        np.savez(path, **{n.replace("/", "__"): v for n, v in self.params.items()})
+        """npz checkpoint: parameters (reference names) + the trainer's Adam state."""
+        path = "%s-%s.npz" % (self.checkpoint_file, step)
+        arrs = {n.replace("/", "__"): v for n, v in self.params.items()}
+        tr = getattr(self, "_tr", None)
+        if tr is not None:
+            st = tr.opt.state()
+            for j, n in enumerate(self.PARAM_NAMES):
+                arrs["adam_m__" + n.replace("/", "__")] = st["m"][j]
+                arrs["adam_v__" + n.replace("/", "__")] = st["v"][j]
+            arrs["adam_b1p"] = np.float32(st["b1p"])
+            arrs["adam_b2p"] = np.float32(st["b2p"])
+        np.savez(path, **arrs)
         return path
 
     def load_checkpoint(self, iter_to_load, do_checks=True):
-        """npz parameter checkpoints written by save_checkpoint (TF checkpoints are not read)."""
-        path = os.path.join(self.train_dir, "%s-checkpoint-%s.npz" % (self.model_name, iter_to_load))
+        """npz checkpoints written by save_checkpoint (saver.restore, gnn:414-420).  TF
+        checkpoints of the reference are read by influence.tf_checkpoint."""
+        path = "%s-%s.npz" % (self.checkpoint_file, iter_to_load)
         with np.load(path, allow_pickle=False) as z:
-            self.load_params({n.replace("__", "/"): z[n] for n in z.files})
+            files = set(z.files)
+            self.load_params({n: z[n.replace("/", "__")] for n in self.PARAM_NAMES})
+            tr = getattr(self, "_tr", None)
+            if tr is not None:
+                tr.set_params(self.params)
+                if "adam_b1p" in files:
+                    tr.opt.load_state({"m": [z["adam_m__" + n.replace("/", "__")] for n in self.PARAM_NAMES],
+                                       "v": [z["adam_v__" + n.replace("/", "__")] for n in self.PARAM_NAMES],
+                                       "b1p": float(z["adam_b1p"]), "b2p": float(z["adam_b2p"])})
+                else:
+                    tr.opt.reset()
         if self.verbose:
             print("Loading successful...")
+
+    def load_tf_checkpoint(self, prefix):
+        """Load a reference TF checkpoint-V2 bundle (tf.train.Saver output, e.g.
+        output/<model_name>-checkpoint-<step>) without TensorFlow: the variables under the
+        reference names, plus the Adam slots <var>/Adam, <var>/Adam_1 and beta powers when
+        present (influence/tf_checkpoint.py)."""
+        from influence import tf_checkpoint as tfc
+        t = tfc.read_checkpoint(prefix)
+        missing = [n for n in self.PARAM_NAMES if n not in t]
+        if missing:
+            raise ValueError("checkpoint %s lacks %s" % (prefix, ", ".join(missing)))
+        self.load_params({n: t[n].reshape(-1) for n in self.PARAM_NAMES})
+        tr = getattr(self, "_tr", None)
+        if tr is not None:
+            tr.set_params(self.params)
+            slots = all(n + "/Adam" in t and n + "/Adam_1" in t for n in self.PARAM_NAMES)
+            if slots and "beta1_power" in t and "beta2_power" in t:
+                tr.opt.load_state({"m": [t[n + "/Adam"].reshape(-1) for n in self.PARAM_NAMES],
+                                   "v": [t[n + "/Adam_1"].reshape(-1) for n in self.PARAM_NAMES],
+                                   "b1p": float(t["beta1_power"]), "b2p": float(t["beta2_power"])})
+            else:
+                tr.opt.reset()
+
+    def save_tf_checkpoint(self, prefix):
+        """Write the parameters (and the trainer's Adam state) as a TF checkpoint-V2 bundle
+        under the reference variable names."""
+        from influence import tf_checkpoint as tfc
+        t = {n: np.asarray(self.params[n], np.float32) for n in self.PARAM_NAMES}
+        tr = getattr(self, "_tr", None)
+        if tr is not None:
+            st = tr.opt.state()
+            for j, n in enumerate(self.PARAM_NAMES):
+                t[n + "/Adam"] = st["m"][j]
+                t[n + "/Adam_1"] = st["v"][j]
+            t["beta1_power"] = np.float32(st["b1p"])
+            t["beta2_power"] = np.float32(st["b2p"])
+        tfc.write_checkpoint(prefix, t)
+        return prefix
+
+    # ---------------------------------------------------------------- training
+    @property
+    def model_kind(self):
+        return "MF" if self.MODEL_ID == _lib.FIA_MODEL_MF else "NCF"
+
+    def trainer(self):
+        """The model's TF-Adam trainer (created on first use from the current params)."""
+        if getattr(self, "_tr", None) is None:
+            from influence.train import Trainer
+            self._tr = Trainer(self.model_kind, self.embedding_size, self.weight_decay, self.initial_learning_rate,
+                               self.params, self.PARAM_NAMES, self.ctx.torch_device)
+        return self._tr
+
+    def _sync_from_trainer(self):
+        """Trained values -> FIA context (re-upload + Hessian caches)."""
+        self.load_params(self.trainer().params_numpy())
+
+    def train(self, num_steps, iter_to_switch_to_batch=10000000, iter_to_switch_to_sgd=10000000,
+              save_checkpoints=True, verbose=True, load_checkpoints=False):
+        """Adam on reference mini-batches (gnn:367-412): steps load_checkpoints+1 .. num_steps-1,
+        then the parameters go to the FIA context and, with save_checkpoints, a checkpoint
+        num_steps-1 is written (the reference saves only past step 20000; this build always
+        saves at the end).  The SGD phase (gnn:395-397) is not used by the reference scripts
+        and is not provided."""
+        if iter_to_switch_to_sgd < num_steps:
+            raise NotImplementedError("the SGD phase of GenericNeuralNet.train is not provided")
+        tr = self.trainer()
+        if load_checkpoints:
+            self.load_checkpoint(load_checkpoints, do_checks=False)
+        else:
+            load_checkpoints = 0
+        train = self.data_sets["train"]
+        full = None
+        ran = False
+        for step in range(load_checkpoints + 1, num_steps):
+            t0 = time.time()
+            if step < iter_to_switch_to_batch:
+                xb, yb = train.next_batch(self.batch_size)
+                loss = tr.step(xb[:, 0].astype(np.int64), xb[:, 1].astype(np.int64), yb)
+            else:
+                if full is None:
+                    full = self.fill_feed_dict_with_all_ex(train)
+                loss = tr.step(full["users"], full["items"], full["labels"])
+            ran = True
+            if verbose and step % 1000 == 0:
+                print("Step %d: loss = %.8f (%.3f sec)" % (step, float(loss), time.time() - t0))
+        if ran:
+            self._sync_from_trainer()
+            if save_checkpoints:
+                self.save_checkpoint(num_steps - 1)
+
+    def fill_feed_dict_with_all_ex(self, data_set):
+        """All rows (gnn:210-215), as index arrays for the trainer."""
+        x = np.asarray(data_set.x)
+        return {"users": x[:, 0].astype(np.int64), "items": x[:, 1].astype(np.int64),
+                "labels": np.asarray(data_set.labels, np.float32)}
+
+    def fill_feed_dict_with_all_but_one_ex(self, data_set, idx_to_remove):
+        """All rows but train row idx_to_remove (gnn:218-227)."""
+        keep = np.ones(data_set.x.shape[0], bool)
+        keep[idx_to_remove] = False
+        x = np.asarray(data_set.x)[keep]
+        return {"users": x[:, 0].astype(np.int64), "items": x[:, 1].astype(np.int64),
+                "labels": np.asarray(data_set.labels, np.float32)[keep]}
+
+    def retrain(self, num_steps, feed_dict):
+        """num_steps full-batch Adam steps on feed_dict's rows (gnn:344-347); one HIP graph
+        replay per step.  Only the trainer's parameters change (the FIA context keeps the
+        loaded model)."""
+        self.trainer().full_batch(feed_dict["users"], feed_dict["items"], feed_dict["labels"], num_steps)
+
+    def reset_optimizer(self):
+        """reset_optimizer_op (gnn:437-438)."""
+        self.trainer().opt.reset()
+
+    def predict_pairs(self, users, items):
+        """Trainer-side r-hat (float64) for (user, item) pairs."""
+        return self.trainer().predict(np.asarray(users, np.int64), np.asarray(items, np.int64))
+
+    def predict_test(self, test_idx):
+        """r-hat of test rating test_idx under the trainer's current parameters (model.logits)."""
+        u, i = self._test_pair(test_idx)
+        return float(self.predict_pairs([u], [i])[0])
+
+    def train_loss(self):
+        """total_loss on all training rows under the trainer's parameters."""
+        f = self.fill_feed_dict_with_all_ex(self.data_sets["train"])
+        return self.trainer().loss(f["users"], f["items"], f["labels"])
 
     # ------------------------------------------------------------------- index
     def _build_index(self, train):
