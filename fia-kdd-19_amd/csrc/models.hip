@@ -535,7 +535,7 @@ struct QueryArgs {
 // !COLS: the full D x D packed LDL^T (coupled queries, or every query of qlist).
 // qlist (nullable): {count, q_0, q_1, ...}.
 template <class M, bool COLS>
-__global__ __launch_bounds__(kSolveThreads) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
+__global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
                                                          double* __restrict__ x_out, const int32_t* __restrict__ qlist,
                                                          int32_t* __restrict__ coupled_out) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
@@ -1699,7 +1699,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                          c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else {
-      const int64_t g1 = Q < 2048 ? Q : 2048;     // persistent: weights staged once per block
+      const int64_t g1 = Q < 8192 ? Q : 8192;     // persistent: weights staged once per block
       hipLaunchKernelGGL((k_solve<M, true>), dim3((unsigned)g1), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
                          x_out, (const int32_t*)nullptr, c->coupled.as<int32_t>());
     }
