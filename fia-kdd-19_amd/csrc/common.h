@@ -28,7 +28,7 @@ struct ChunkDesc {
 };
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
-constexpr int kGramChunk = 512;          // list rows per Gram work item
+constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item
 
 // Device buffer with grow-on-demand capacity (never shrinks).

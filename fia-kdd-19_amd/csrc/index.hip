@@ -8,6 +8,7 @@
 // ascending order, so rel(u,i) = R_u ++ C_i is the reference's concatenation
 // bit for bit (mf:322).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -224,6 +225,16 @@ __global__ void k_write_related(const int32_t* __restrict__ qu, const int32_t* _
   for (int64_t p = threadIdx.x; p < di; p += blockDim.x) rel[base + du + p] = irow[ib + p];
 }
 
+// list rows per small-k Gram work item (FIA_GRAM_CHUNK overrides, for A/B runs)
+inline int64_t gram_chunk() {
+  static const int64_t v = [] {
+    const char* e = getenv("FIA_GRAM_CHUNK");
+    const long long x = e ? atoll(e) : 0;
+    return (int64_t)(x >= 32 ? x : kGramChunk);
+  }();
+  return v;
+}
+
 inline unsigned bits_for(int64_t n) {
   unsigned b = 1;
   while (b < 31 && ((int64_t)1 << b) < n) ++b;
@@ -311,11 +322,12 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
     int32_t slots = 0;
     for (int32_t e : ord) {
       const int64_t len = hptr[(size_t)e + 1] - hptr[(size_t)e];
-      const int64_t nit = len == 0 ? 1 : (len + kGramChunk - 1) / kGramChunk;
+      const int64_t gch = gram_chunk();
+      const int64_t nit = len == 0 ? 1 : (len + gch - 1) / gch;
       if (nit > 1) comb.insert(comb.end(), {e, slots, (int32_t)nit, 0});
       for (int64_t t = 0; t < nit; ++t) {
-        const int64_t st = t * kGramChunk;
-        const int64_t ln = std::min<int64_t>(kGramChunk, len - st);
+        const int64_t st = t * gch;
+        const int64_t ln = std::min<int64_t>(gch, len - st);
         items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), nit > 1 ? slots++ : -1});
       }
     }

@@ -905,18 +905,32 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
 // ------------------------------------------------------------------------------------
 typedef double d4_t __attribute__((ext_vector_type(4)));
 
+// both sides' Gram work in one launch: blocks [0, n_items[0]) users, the rest items
+struct GramSides {
+  int64_t n_items[2];
+  const int32_t* items[2];
+  const int64_t* ptr[2];
+  const int32_t* other[2];
+  const float* emb_other[2];
+  double* gram[2];
+  double* part[2];
+};
+
 template <class M>
-__global__ __launch_bounds__(64) void k_gram_mf_mfma(int64_t n_items, const int32_t* __restrict__ items,
-                                                     const int64_t* __restrict__ ptr,
-                                                     const int32_t* __restrict__ other,
-                                                     const float* __restrict__ emb_other, double* __restrict__ gram,
-                                                     double* __restrict__ part) {
+__global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
   constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   constexpr int NT = (K + 15) / 16;               // 16-wide column tiles
   constexpr int NP = NT * (NT + 1) / 2;           // upper tile pairs
   constexpr int SUB = NT <= 2 ? 16 : 8;           // MFMA row-quads gathered ahead per batch
-  const int64_t w = blockIdx.x;
-  if (w >= n_items) return;
+  const int sd = (int64_t)blockIdx.x >= GSd.n_items[0] ? 1 : 0;
+  const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
+  if (w >= GSd.n_items[sd]) return;
+  const int32_t* __restrict__ items = GSd.items[sd];
+  const int64_t* __restrict__ ptr = GSd.ptr[sd];
+  const int32_t* __restrict__ other = GSd.other[sd];
+  const float* __restrict__ emb_other = GSd.emb_other[sd];
+  double* __restrict__ gram = GSd.gram[sd];
+  double* __restrict__ part = GSd.part[sd];
   const int32_t e = items[4 * w], start = items[4 * w + 1], len = items[4 * w + 2], slot = items[4 * w + 3];
   const int lane = threadIdx.x;
   const int col = lane & 15, grp = lane >> 4;
@@ -1093,12 +1107,19 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
   }
 }
 
-// Sum the partial Grams of split lists in slot order (deterministic).
-__global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb, const int32_t* __restrict__ comb, int GS,
-                                                     int GSP, const double* __restrict__ part,
-                                                     double* __restrict__ gram) {
-  const int64_t w = blockIdx.x;
-  if (w >= n_comb) return;
+// Sum the partial Grams of split lists in slot order (deterministic); both sides in one
+// launch (blocks [0, n_comb0) the user side).
+__global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int32_t* __restrict__ comb0,
+                                                     const double* __restrict__ part0, double* __restrict__ gram0,
+                                                     int64_t n_comb1, const int32_t* __restrict__ comb1,
+                                                     const double* __restrict__ part1, double* __restrict__ gram1,
+                                                     int GS, int GSP) {
+  const int sd = (int64_t)blockIdx.x >= n_comb0 ? 1 : 0;
+  const int64_t w = (int64_t)blockIdx.x - (sd ? n_comb0 : 0);
+  if (w >= (sd ? n_comb1 : n_comb0)) return;
+  const int32_t* __restrict__ comb = sd ? comb1 : comb0;
+  const double* __restrict__ part = sd ? part1 : part0;
+  double* __restrict__ gram = sd ? gram1 : gram0;
   const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
   for (int t = threadIdx.x; t < GS; t += 64) {
     double s = 0.0;
@@ -1279,6 +1300,147 @@ __global__ __launch_bounds__(kScoreThreads) void k_score(
         pp = bp;
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// MF per-query-chunk scoring, software-pipelined across the wave's chunks.  A chunk's
+// critical path is three dependent round trips (descriptor -> list entries + record ->
+// gathered rows); here the next chunk's descriptor, list entries and record words are
+// loaded while the current chunk's gathers are in flight, so each chunk waits on one
+// round trip.  Same arithmetic (and bits) as k_score.
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(kScoreThreads) void k_score_mf(
+    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(!M::ncf, "MF scoring");
+  constexpr int K = M::K, RT = kScoreRows, NV = (M::SB + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nchunks = coff[Q];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  struct Stage {
+    ChunkDesc d;
+    int32_t o[RT], row[RT];
+    float y[RT];
+    double hv, rv[NV];
+  };
+  auto fetch = [&](int64_t c, Stage& st) {
+    st.d = cdesc[c];
+    const int sd = st.d.side;
+    const int32_t* __restrict__ oth = A.other[sd] + st.d.list_base;
+    const float* __restrict__ rat = A.rating[sd] + st.d.list_base;
+    const int32_t* __restrict__ rw = A.row[sd] + st.d.list_base;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int idx = r * 64 + lane;
+      const int li = idx < st.d.len ? idx : 0;
+      st.o[r] = oth[li];
+      st.y[r] = rat[li];
+      st.row[r] = rw[li];
+    }
+    const double* __restrict__ R = rec + (int64_t)st.d.q * M::R;
+    const double* __restrict__ Sg = R + 4 + sd * M::SB;
+    st.hv = R[lane & 3];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) st.rv[v] = Sg[v * 64 + lane < M::SB ? v * 64 + lane : M::SB - 1];
+  };
+  int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave;
+  Stage cur;
+  if (ch < nchunks) fetch(ch, cur);
+  while (ch < nchunks) {
+    const int sd = cur.d.side;
+    // gathers of the current chunk
+    float4 g4_[RT][K / 4];
+    float gb_[RT];
+    {
+      const float* T = sd == 0 ? A.t[1] : A.t[0];
+      const float* bt = sd == 0 ? A.t[3] : A.t[2];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)cur.o[r] * K);
+#pragma unroll
+        for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
+        gb_[r] = bt[cur.o[r]];
+      }
+    }
+    // next chunk's descriptor, list entries and record, behind the gathers
+    const int64_t nx = ch + stride;
+    Stage nxt;
+    if (nx < nchunks) fetch(nx, nxt);
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+#pragma unroll
+      for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
+      asm volatile("" ::"v"(gb_[r]));
+    }
+    const ChunkDesc& d = cur.d;
+    const double inv_n = readlane_d(cur.hv, 0), cq = readlane_d(cur.hv, 1), xv = readlane_d(cur.hv, 2),
+                 rhat_ui = readlane_d(cur.hv, 3);
+#define RS(c) readlane_d(cur.rv[(c) / 64], (c) % 64)
+    double dot_a[RT], dot_x[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) dot_a[r] = dot_x[r] = 0.0;
+#pragma unroll
+    for (int c4 = 0; c4 < K / 4; ++c4) {
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const double ac = RS(4 * c4 + cc), xc = RS(K + 4 * c4 + cc);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const float4 t = g4_[r][c4];
+          const double tv = (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w);
+          dot_a[r] = fma(ac, tv, dot_a[r]);
+          dot_x[r] = fma(xc, tv, dot_x[r]);
+        }
+      }
+    }
+    const double bias_s = RS(2 * K), xsb = RS(2 * K + 1), dup_o = RS(2 * K + 2);
+#undef RS
+    double ca[RT], cv[RT];
+    int cp[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int idx = r * 64 + lane;
+      const bool ok = idx < d.len;
+      const double y = (double)cur.y[r];
+      double e = dot_a[r] + bias_s + (double)gb_[r] - y;
+      double s = dot_x[r] + xsb;
+      if ((double)cur.o[r] == dup_o) { e = rhat_ui - y; s = xv; }
+      const double infl = (2.0 * e * s + cq) * inv_n;
+      if (ok) {
+        if (influence) __builtin_nontemporal_store(infl, influence + d.out_base + idx);
+        if (rel_idx) __builtin_nontemporal_store((int64_t)cur.row[r], rel_idx + d.out_base + idx);
+      }
+      cp[r] = ok ? d.pos0 + idx : -1;
+      ca[r] = ok ? topk_key(infl) : -2.0;
+      cv[r] = infl;
+    }
+    if (K_top > 0) {
+      double pa = INFINITY;
+      int pp = -1;
+      for (int t = 0; t < K_top; ++t) {
+        double ba = -2.0, bv = 0.0;
+        int bp = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
+            ba = ca[r]; bp = cp[r]; bv = cv[r];
+          }
+        wave_best(ba, bp, bv);
+        if (lane == 0) {
+          const bool okk = ba > -1.5;
+          cand_pos[ch * K_top + t] = okk ? bp : -1;
+          cand_val[ch * K_top + t] = okk ? bv : NAN;
+        }
+        pa = ba;
+        pp = bp;
+      }
+    }
+    cur = nxt;
+    ch = nx;
   }
 }
 
@@ -1634,33 +1796,45 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
       }
     }
   }
-  for (int sd = 0; sd < 2; ++sd) {
-    if (n_ent[sd] == 0) continue;
-    constexpr int GSP = (GS + 1) & ~1;
-    const Index& X = c->idx;
+  constexpr int GSP = (GS + 1) & ~1;
+  const Index& X = c->idx;
+  for (int sd = 0; sd < 2; ++sd)
     if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
-    if (X.n_gitems[sd] > 0) {
-      if constexpr (M::ncf) {
-        constexpr int WAVES = NCFGramCfg<M>::WAVES;
-        int64_t grid = (X.n_gitems[sd] + WAVES - 1) / WAVES;
-        if (grid > 16384) grid = 16384;
-        hipLaunchKernelGGL(k_gram_ncf_mfma<M>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, sd, X.n_gitems[sd],
-                           X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
-                           c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4],
-                           c->p.t[5], c->p.t[6], c->p.t[7], c->p.t[8], c->gram[sd].as<double>(),
-                           c->gpart[sd].as<double>());
-      } else {
-        hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)X.n_gitems[sd]), dim3(64), 0, s, X.n_gitems[sd],
-                           X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
-                           c->p.t[sd == 0 ? 1 : 0], c->gram[sd].as<double>(), c->gpart[sd].as<double>());
-      }
+  if constexpr (M::ncf) {
+    for (int sd = 0; sd < 2; ++sd) {
+      if (n_ent[sd] == 0 || X.n_gitems[sd] == 0) continue;
+      constexpr int WAVES = NCFGramCfg<M>::WAVES;
+      int64_t grid = (X.n_gitems[sd] + WAVES - 1) / WAVES;
+      if (grid > 16384) grid = 16384;
+      hipLaunchKernelGGL(k_gram_ncf_mfma<M>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, sd, X.n_gitems[sd],
+                         X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
+                         c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4],
+                         c->p.t[5], c->p.t[6], c->p.t[7], c->p.t[8], c->gram[sd].as<double>(),
+                         c->gpart[sd].as<double>());
       FIA_HIP_TRY(hipGetLastError());
     }
-    if (X.n_gcomb[sd] > 0) {
-      hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)X.n_gcomb[sd]), dim3(64), 0, s, X.n_gcomb[sd],
-                         X.gcomb[sd].as<int32_t>(), GS, GSP, c->gpart[sd].as<double>(), c->gram[sd].as<double>());
+  } else {
+    GramSides G;
+    for (int sd = 0; sd < 2; ++sd) {
+      G.n_items[sd] = n_ent[sd] > 0 ? X.n_gitems[sd] : 0;
+      G.items[sd] = X.gitems[sd].as<int32_t>();
+      G.ptr[sd] = X.side[sd].ptr.as<int64_t>();
+      G.other[sd] = X.side[sd].other.as<int32_t>();
+      G.emb_other[sd] = c->p.t[sd == 0 ? 1 : 0];
+      G.gram[sd] = c->gram[sd].as<double>();
+      G.part[sd] = c->gpart[sd].as<double>();
+    }
+    if (G.n_items[0] + G.n_items[1] > 0) {
+      hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
       FIA_HIP_TRY(hipGetLastError());
     }
+  }
+  const int64_t nc0 = n_ent[0] > 0 ? X.n_gcomb[0] : 0, nc1 = n_ent[1] > 0 ? X.n_gcomb[1] : 0;
+  if (nc0 + nc1 > 0) {
+    hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)(nc0 + nc1)), dim3(64), 0, s, nc0, X.gcomb[0].as<int32_t>(),
+                       c->gpart[0].as<double>(), c->gram[0].as<double>(), nc1, X.gcomb[1].as<int32_t>(),
+                       c->gpart[1].as<double>(), c->gram[1].as<double>(), GS, GSP);
+    FIA_HIP_TRY(hipGetLastError());
   }
   return hipSuccess;
 }
@@ -1695,9 +1869,11 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
   FIA_HIP_TRY(hipMemsetAsync(c->coupled.ptr, 0, sizeof(int32_t), s));
   if (Q > 0) {
-    if constexpr (use_tps<M>()) {
-      hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
-                         c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+    static const bool tps_on = !getenv("FIA_NO_TPS");   // A/B knob: wave-per-query solve instead
+    if (use_tps<M>() && tps_on) {
+      if constexpr (use_tps<M>())
+        hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
+                           c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else {
       const int64_t g1 = Q < 8192 ? Q : 8192;     // persistent: weights staged once per block
       hipLaunchKernelGGL((k_solve<M, true>), dim3((unsigned)g1), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
@@ -1720,9 +1896,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                        c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
                        c->cand_val.as<double>());
   } else {
-    hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(),
-                       c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence, K,
-                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+    if constexpr (!M::ncf) {
+      hipLaunchKernelGGL(k_score_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q,
+                         c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence,
+                         K, c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+    } else {
+      hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(),
+                         c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence, K,
+                         c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+    }
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);

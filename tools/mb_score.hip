@@ -248,21 +248,19 @@ int main() {
     printf("%-34s grid %6d  %8.1f us  %6.2f TB/s (28 B/row)\n", name, (int)(grid), ms * 1e3, bytes / (ms * 1e-3) / 1e12); \
   }
   RUN("v0 RW4", (k_v0<4, 0>), 4, 8192);
-  RUN("v0 RW8", (k_v0<8, 0>), 8, 8192);
-  RUN("v0 RW4 no stores", (k_v0<4, 4>), 4, 8192);
   RUN("v0 RW4 nt stores", (k_v0<4, 32>), 4, 8192);
-  RUN("v0 RW4 sc1 stores", (k_v0<4, 64>), 4, 8192);
-  RUN("v0 RW4 nt loads", (k_v0<4, 128>), 4, 8192);
-  RUN("v0 RW4 nt loads+stores", (k_v0<4, 160>), 4, 8192);
-  RUN("v0 RW4 infl only", (k_v0<4, 256>), 4, 8192);
+  RUN("v0 RW4 gather row0", (k_v0<4, 1>), 4, 8192);
+  RUN("v0 RW4 no gathers", (k_v0<4, 8>), 4, 8192);
+  RUN("v0 RW4 no stores", (k_v0<4, 4>), 4, 8192);
+  RUN("v0 RW4 no gathers no stores", (k_v0<4, 12>), 4, 8192);
+  RUN("v0 RW4 fp32 math", (k_v0<4, 2>), 4, 8192);
+  RUN("v0 RW4 padded table", (k_v0<4, 16>), 4, 8192);
+  RUN("quad", (k_quad<0>), 4, 8192);
+  RUN("quad no stores", (k_quad<4>), 4, 8192);
+  RUN("quad row0", (k_quad<1>), 4, 8192);
   RUN("v0 RW8 nt stores", (k_v0<8, 32>), 8, 8192);
-  RUN("v0 RW8 nt loads+stores", (k_v0<8, 160>), 8, 8192);
-  RUN("v0 RW8 sc1 stores", (k_v0<8, 64>), 8, 8192);
-  RUN("v0 RW8 no stores", (k_v0<8, 4>), 8, 8192);
-  RUN("v0 RW8 gather row0", (k_v0<8, 1>), 8, 8192);
-  RUN("v0 RW6", (k_v0<6, 0>), 6, 8192);
-  RUN("v0 RW6 nt stores", (k_v0<6, 32>), 6, 8192);
-  RUN("v0 RW8 grid 4096", (k_v0<8, 0>), 8, 4096);
-  RUN("v0 RW8 grid 16384", (k_v0<8, 0>), 8, 16384);
+  RUN("v0 RW2 nt stores", (k_v0<2, 32>), 2, 8192);
+  RUN("v0 RW4 nt grid 2048", (k_v0<4, 32>), 4, 2048);
+  RUN("v0 RW4 nt grid 32768", (k_v0<4, 32>), 4, 32768);
   return 0;
 }
