@@ -126,7 +126,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from influence import _lib
-    from influence.sharding import gather_topk
+    from influence.sharding import TopKGather, shard_ranges
 
     d, params = load_data(cfg)
     tu, ti, tr = d["train"]
@@ -152,9 +152,11 @@ def main():
     qi = torch.from_numpy(qi_np).to(dev)
     offsets_all, _ = ctx.count_related(qu, qi)
     n_q = np.diff(offsets_all.cpu().numpy())
+    all_sizes = [int(n_q.size)] * world        # weak scaling: every rank answers one full set
     if args.shard_of > 1:
-        from influence.sharding import shard_ranges
-        b0, b1 = shard_ranges(n_q, args.shard_of)[rank % args.shard_of]
+        rs = shard_ranges(n_q, args.shard_of)
+        all_sizes = [rs[r % args.shard_of][1] - rs[r % args.shard_of][0] for r in range(world)]
+        b0, b1 = rs[rank % args.shard_of]
         qu_np, qi_np, n_q = qu_np[b0:b1], qi_np[b0:b1], n_q[b0:b1]
         qu, qi = qu[b0:b1].contiguous(), qi[b0:b1].contiguous()
     Q = int(qu_np.size)
@@ -185,6 +187,9 @@ def main():
 
     big_k = k >= 128 or (cfg["model"] == "NCF" and k >= 64)
 
+    # the top-K exchange: one async all_gather per step, overlapped with the next step
+    tg = TopKGather(all_sizes, K, dev) if world > 1 else None
+
     def step():
         if big_k:
             ctx.prepare_for(qu, qi)    # caches for this GPU's users/items only (fia_prepare_for)
@@ -194,11 +199,13 @@ def main():
             ctx.count_related(qb_u, qb_i, off_b, want_total=False)
             ctx.query_batch(qb_u, qb_i, off_b, tot_b, rel, infl, xbuf, K, tp[b0 * K:b1 * K],
                             tix[b0 * K:b1 * K], tv[b0 * K:b1 * K])
-        if world > 1:
-            gather_topk(tix.view(Q, K), tv.view(Q, K))
+        if tg is not None:
+            tg.start(tix.view(Q, K), tv.view(Q, K))
 
     for _ in range(args.warmup):
         step()
+    if tg is not None:
+        tg.wait()
     torch.cuda.synchronize(dev)
     ctx.profile_read()
     ctx.set_profiling(True)
@@ -208,6 +215,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if tg is not None:
+        tg.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -27,21 +27,22 @@ def shard_ranges(costs, world_size):
     return [(bounds[r], bounds[r + 1]) for r in range(world_size)]
 
 
-def gather_topk(topk_idx, topk_val, group=None):
+def gather_topk(topk_idx, topk_val, group=None, sizes=None):
     """All ranks' [Q_r, K] top-K lists, concatenated in rank order on every rank.
 
     topk_idx: int64 tensor [Q_r, K]; topk_val: float64 tensor [Q_r, K] (same device
     as the process group's backend expects: cuda for nccl/RCCL, cpu for gloo).
     Shards may differ in Q_r: rows are padded to the largest shard, gathered, and
-    the padding is dropped."""
+    the padding is dropped.  sizes (every rank's Q_r) skips the size exchange."""
     import torch
     import torch.distributed as dist
     ws = dist.get_world_size(group)
     K = topk_idx.shape[1] if topk_idx.dim() == 2 else 1
-    q_local = torch.tensor([topk_idx.shape[0]], dtype=torch.int64, device=topk_idx.device)
-    sizes = [torch.zeros_like(q_local) for _ in range(ws)]
-    dist.all_gather(sizes, q_local, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        q_local = torch.tensor([topk_idx.shape[0]], dtype=torch.int64, device=topk_idx.device)
+        sz = [torch.zeros_like(q_local) for _ in range(ws)]
+        dist.all_gather(sz, q_local, group=group)
+        sizes = [int(s.item()) for s in sz]
     qmax = max(sizes) if sizes else 0
     # pack idx and value bits into one int64 [Q, 2K] buffer: one collective
     pack = torch.full((qmax, 2 * K), -1, dtype=torch.int64, device=topk_idx.device)
@@ -53,3 +54,54 @@ def gather_topk(topk_idx, topk_val, group=None):
     parts = [b[:s] for b, s in zip(bufs, sizes)]
     allp = torch.cat(parts, 0) if parts else pack[:0]
     return allp[:, :K].contiguous(), allp[:, K:].contiguous().view(torch.float64)
+
+
+class TopKGather(object):
+    """The per-step top-K exchange of a multi-GPU job, asynchronous and double-buffered.
+
+    Shard sizes are known up front (contiguous ranges from shard_ranges, or equal
+    per-GPU batches), so there is no size exchange: start() packs this rank's
+    [Q_r, K] lists (int64 index + float64 bits) into one of two persistent buffers
+    and launches one all_gather with async_op=True, which overlaps the next step's
+    kernels on the compute stream (RCCL runs on its own stream).  A buffer is
+    reused only after its previous collective completed; wait() drains both and
+    returns the gathered [sum Q_r, K] lists of the last start()."""
+
+    def __init__(self, sizes, K, device, group=None):
+        import torch
+        self.sizes = [int(x) for x in sizes]
+        self.K = int(K)
+        self.group = group
+        qmax = max(self.sizes) if self.sizes else 0
+        self.pack = [torch.full((max(qmax, 1), 2 * self.K), -1, dtype=torch.int64, device=device) for _ in range(2)]
+        self.bufs = [[torch.empty_like(self.pack[j]) for _ in self.sizes] for j in range(2)]
+        self.work = [None, None]
+        self.slot = 0
+        self.last = None
+
+    def start(self, topk_idx, topk_val):
+        import torch.distributed as dist
+        j = self.slot
+        self.slot ^= 1
+        if self.work[j] is not None:
+            self.work[j].wait()
+        n = topk_idx.shape[0]
+        p = self.pack[j]
+        if n:
+            p[:n, :self.K] = topk_idx.reshape(-1, self.K)
+            p[:n, self.K:] = topk_val.reshape(-1, self.K).contiguous().view(p.dtype)
+        self.work[j] = dist.all_gather(self.bufs[j], p, group=self.group, async_op=True)
+        self.last = j
+        return j
+
+    def wait(self):
+        import torch
+        for j in range(2):
+            if self.work[j] is not None:
+                self.work[j].wait()
+                self.work[j] = None
+        if self.last is None:
+            return None, None
+        parts = [b[:s] for b, s in zip(self.bufs[self.last], self.sizes)]
+        allp = torch.cat(parts, 0)
+        return allp[:, :self.K].contiguous(), allp[:, self.K:].contiguous().view(torch.float64)

@@ -43,7 +43,16 @@ def _worker(rank, ws, port, qs, K, out):
         idx = torch.tensor(np.stack([q * 10 + j for j in range(K)], 1), dtype=torch.int64).reshape(-1, K)
         val = torch.tensor(np.stack([np.sin(q + j) for j in range(K)], 1), dtype=torch.float64).reshape(-1, K)
         gi, gv = gather_topk(idx, val)
-        out[rank] = (gi.numpy().copy(), gv.numpy().copy())
+        # known sizes: no size exchange; and the async double-buffered form over 3 "steps"
+        sizes = [e2 - b2 for b2, e2 in rs]
+        gi2, gv2 = gather_topk(idx, val, sizes=sizes)
+        from influence.sharding import TopKGather
+        tg = TopKGather(sizes, K, "cpu")
+        for step in range(3):
+            tg.start(idx + 1000 * step, val + step)
+        gi3, gv3 = tg.wait()
+        assert np.array_equal(gi2.numpy(), gi.numpy()) and np.array_equal(gv2.numpy(), gv.numpy())
+        out[rank] = (gi.numpy().copy(), gv.numpy().copy(), gi3.numpy().copy() - 2000, gv3.numpy().copy() - 2)
     finally:
         dist.destroy_process_group()
 
@@ -60,6 +69,8 @@ def test_gather_topk_gloo_world2(qs):
     want_i = np.stack([q * 10 + j for j in range(K)], 1)
     want_v = np.stack([np.sin(q + j) for j in range(K)], 1)
     for r in range(ws):
-        gi, gv = res[r]
+        gi, gv, gi3, gv3 = res[r]
         assert np.array_equal(gi, want_i)
         assert np.array_equal(gv, want_v)
+        assert np.array_equal(gi3, want_i)          # the last async step's lists
+        assert np.allclose(gv3, want_v, atol=1e-12)
