@@ -857,7 +857,7 @@ __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __re
 
 // ------------------------------------------------------------------------------------
 // Entity-shared scoring (work items from build_groups: one <= kChunk chunk of one
-// entity's list x one block of <= kQueryBlock queries with that entity).  Per rating:
+// entity's list x one block of <= kBigQueryBlock queries with that entity).  Per rating:
 //   MF  s_q = x_emb,q . emb_other + x_bias,q
 //   NCF s_q = x_mlp,q . g_mlp,j + (W3g * x_gmf,q) . gmf_other
 //   influence = (2 e_j s_q + c_q) / n_q   (mf:240-246); the test pair's own train row
@@ -865,7 +865,7 @@ __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __re
 // ------------------------------------------------------------------------------------
 template <class M>
 constexpr int score_waves() {
-  return (4 + M::SB) * kQueryBlock * 8 > 20000 ? 2 : 4;
+  return (4 + M::SB) * kBigQueryBlock * 8 > 20000 ? 2 : 4;
 }
 
 template <class M>
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  constexpr int K = M::K, SW = score_waves<M>(), QB = kQueryBlock, RSW = 4 + M::SB;
+  constexpr int K = M::K, SW = score_waves<M>(), QB = kBigQueryBlock, RSW = 4 + M::SB;
   constexpr int NPASS = kScoreRows;
   __shared__ double srec[SW][QB * RSW];
   __shared__ int64_t sbase[SW][3 * QB];
@@ -1054,19 +1054,6 @@ int cu_count(fia_ctx* c) {
 hipError_t big_work_lists(fia_ctx* c, const std::vector<uint8_t>* marks) {
   Index& X = c->idx;
   if (!marks && !c->subset && c->bitems_version == X.version) return hipSuccess;
-  if (c->border_version != X.version) {
-    for (int sd = 0; sd < 2; ++sd) {
-      const std::vector<int64_t>& hp = X.hptr[sd];
-      const int64_t ne = (int64_t)hp.size() - 1;
-      std::vector<int32_t>& ord = c->border[sd];
-      ord.resize((size_t)ne);
-      for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = (int32_t)e;
-      std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
-        return hp[(size_t)a + 1] - hp[(size_t)a] > hp[(size_t)b + 1] - hp[(size_t)b];
-      });
-    }
-    c->border_version = X.version;
-  }
   for (int sd = 0; sd < 2; ++sd) {
     const std::vector<int64_t>& hp = X.hptr[sd];
     const int64_t ne = (int64_t)hp.size() - 1;
@@ -1076,7 +1063,7 @@ hipError_t big_work_lists(fia_ctx* c, const std::vector<uint8_t>* marks) {
       if (!marks || marks[sd][(size_t)e]) slot[(size_t)e] = ncache++;
     std::vector<int32_t> items, comb;
     int32_t parts = 0;
-    for (int32_t e : c->border[sd]) {
+    for (int32_t e : X.hord[sd]) {
       if (slot[(size_t)e] < 0) continue;
       const int64_t len = hp[(size_t)e + 1] - hp[(size_t)e];
       const int64_t nit = len == 0 ? 1 : (len + kBigSlice - 1) / kBigSlice;
@@ -1224,7 +1211,7 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   const BigArgs A = make_big_args(c, qu, qi);
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, true, s));
-  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, s));
+  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, kBigQueryBlock, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   FIA_HIP_TRY(hipMemsetAsync(c->syslist.ptr, 0, sizeof(int32_t), s));

@@ -29,7 +29,8 @@ struct ChunkDesc {
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
-constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item
+constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
+constexpr int kBigQueryBlock = 8;        // ... large k (register-resident per-query sums)
 
 // Device buffer with grow-on-demand capacity (never shrinks).
 struct DevBuf {
@@ -84,7 +85,9 @@ struct Index {
   DevBuf pcnt;    // int32  [pcap]
   DevBuf psum;    // double [pcap]
   int64_t pcap = 0;
-  std::vector<int64_t> hptr[2];   // host copies of side[s].ptr (large-k Gram work lists)
+  std::vector<int64_t> hptr[2];   // host copies of side[s].ptr (Gram work lists)
+  std::vector<int32_t> hord[2];   // entities by list length, longest first (host)
+  int64_t gchunk = 0;             // list rows per small-k Gram work item of gitems
   uint64_t version = 0;           // bumped by every build_index
   bool valid = false;
 };
@@ -175,8 +178,6 @@ struct fia_ctx {
   bool subset = false;    // caches cover only the fia_prepare_for entities (large-k models)
   fia::DevBuf bitems[2], bcomb[2];   // large-k Gram work lists {entity, start, len, slot}
   int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0}, n_bcache[2] = {0, 0};
-  std::vector<int32_t> border[2];   // entities by list length, longest first (host)
-  uint64_t border_version = ~0ull;
   uint64_t bitems_version = ~0ull;
   int bitems_k = 0;
   fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta
@@ -202,10 +203,12 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 // per-query chunk offsets coff (+ chunk descriptors unless offsets_only)
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s);
+hipError_t build_gram_lists(fia_ctx* c, int64_t chunk);
+int64_t gram_chunk(int64_t want);
 hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_items, hipStream_t s);
+                        int64_t max_items, int qb, hipStream_t s);
 
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported);

@@ -174,7 +174,7 @@ __global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __re
                              const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
                              const int64_t* __restrict__ gstart, const int32_t* __restrict__ grank,
                              const unsigned long long* __restrict__ gcnt, int32_t* __restrict__ gq,
-                             int64_t* __restrict__ wcnt) {
+                             int64_t* __restrict__ wcnt, int qb) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < Q && grank[2 * t] >= 0) {
     const int32_t u = qu[t], i = qi[t];
@@ -184,7 +184,7 @@ __global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __re
   const int64_t nE = U + I;
   if (t < nE) {
     const int64_t deg = t < U ? uptr[t + 1] - uptr[t] : iptr[t - U + 1] - iptr[t - U];
-    wcnt[t] = gcnt[t] > 0 ? ((deg + kChunk - 1) / kChunk) * (((int64_t)gcnt[t] + kQueryBlock - 1) / kQueryBlock) : 0;
+    wcnt[t] = gcnt[t] > 0 ? ((deg + kChunk - 1) / kChunk) * (((int64_t)gcnt[t] + qb - 1) / qb) : 0;
   } else if (t == nE) {
     wcnt[nE] = 0;
   }
@@ -193,7 +193,7 @@ __global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __re
 // thread per work item (grid-stride up to wstart[nE]): its entity by binary search over
 // wstart, then {entity, chunk of the entity's list, block of the entity's query group}
 __global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned long long* __restrict__ gcnt,
-                            int64_t nE, int32_t* __restrict__ witems) {
+                            int64_t nE, int32_t* __restrict__ witems, int qb) {
   const int64_t total = wstart[nE];
   for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total;
        w += (int64_t)gridDim.x * blockDim.x) {
@@ -203,7 +203,7 @@ __global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned l
       if (wstart[mid] <= w) lo = mid; else hi = mid - 1;
     }
     const int64_t b = wstart[lo];
-    const int64_t nqb = ((int64_t)gcnt[lo] + kQueryBlock - 1) / kQueryBlock;
+    const int64_t nqb = ((int64_t)gcnt[lo] + qb - 1) / qb;
     witems[3 * w] = (int32_t)lo;
     witems[3 * w + 1] = (int32_t)((w - b) / nqb);    // chunk of the entity's list
     witems[3 * w + 2] = (int32_t)((w - b) % nqb);    // block of the entity's query group
@@ -225,15 +225,19 @@ __global__ void k_write_related(const int32_t* __restrict__ qu, const int32_t* _
   for (int64_t p = threadIdx.x; p < di; p += blockDim.x) rel[base + du + p] = irow[ib + p];
 }
 
-// list rows per small-k Gram work item (FIA_GRAM_CHUNK overrides, for A/B runs)
-inline int64_t gram_chunk() {
-  static const int64_t v = [] {
+}  // namespace
+
+// list rows per small-k Gram work item: `want` (the model's choice), FIA_GRAM_CHUNK
+// overrides for A/B runs
+int64_t gram_chunk(int64_t want) {
+  static const long long env = [] {
     const char* e = getenv("FIA_GRAM_CHUNK");
-    const long long x = e ? atoll(e) : 0;
-    return (int64_t)(x >= 32 ? x : kGramChunk);
+    return e ? atoll(e) : 0LL;
   }();
-  return v;
+  return env >= 32 ? (int64_t)env : want;
 }
+
+namespace {
 
 inline unsigned bits_for(int64_t n) {
   unsigned b = 1;
@@ -256,6 +260,41 @@ hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64
   FIA_HIP_TRY(c->scan_tmp.reserve(tb + 16));
   size_t tb2 = c->scan_tmp.bytes;
   return rocprim::exclusive_scan(c->scan_tmp.ptr, tb2, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), s);
+}
+
+// Small-k Gram work lists of the current index: items of <= chunk list rows {entity,
+// start, len, slot} (longest lists first), slot < 0 = write the Gram directly, else a
+// partial slot; a combine entry {entity, first slot, n slots, 0} per split entity.
+hipError_t build_gram_lists(fia_ctx* c, int64_t chunk) {
+  Index& X = c->idx;
+  for (int sd = 0; sd < 2; ++sd) {
+    const std::vector<int64_t>& hptr = X.hptr[sd];
+    std::vector<int32_t> items, comb;
+    int32_t slots = 0;
+    for (int32_t e : X.hord[sd]) {
+      const int64_t len = hptr[(size_t)e + 1] - hptr[(size_t)e];
+      const int64_t nit = len == 0 ? 1 : (len + chunk - 1) / chunk;
+      if (nit > 1) comb.insert(comb.end(), {e, slots, (int32_t)nit, 0});
+      for (int64_t t = 0; t < nit; ++t) {
+        const int64_t st = t * chunk;
+        const int64_t ln = std::min<int64_t>(chunk, len - st);
+        items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), nit > 1 ? slots++ : -1});
+      }
+    }
+    X.n_gitems[sd] = (int64_t)items.size() / 4;
+    X.n_gcomb[sd] = (int64_t)comb.size() / 4;
+    X.n_gslots[sd] = slots;
+    if (!items.empty()) {
+      FIA_HIP_TRY(X.gitems[sd].reserve(sizeof(int32_t) * items.size()));
+      FIA_HIP_TRY(hipMemcpy(X.gitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+    }
+    if (!comb.empty()) {
+      FIA_HIP_TRY(X.gcomb[sd].reserve(sizeof(int32_t) * comb.size()));
+      FIA_HIP_TRY(hipMemcpy(X.gcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
+    }
+  }
+  X.gchunk = chunk;
+  return hipSuccess;
 }
 
 hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* user, const int32_t* item,
@@ -317,30 +356,9 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
     X.hptr[sd] = hptr;
     FIA_HIP_TRY(X.order[sd].reserve(sizeof(int32_t) * ord.size()));
     FIA_HIP_TRY(hipMemcpy(X.order[sd].ptr, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice));
-    // Gram work items (longest lists first) and the combine list of split entities
-    std::vector<int32_t> items, comb;
-    int32_t slots = 0;
-    for (int32_t e : ord) {
-      const int64_t len = hptr[(size_t)e + 1] - hptr[(size_t)e];
-      const int64_t gch = gram_chunk();
-      const int64_t nit = len == 0 ? 1 : (len + gch - 1) / gch;
-      if (nit > 1) comb.insert(comb.end(), {e, slots, (int32_t)nit, 0});
-      for (int64_t t = 0; t < nit; ++t) {
-        const int64_t st = t * gch;
-        const int64_t ln = std::min<int64_t>(gch, len - st);
-        items.insert(items.end(), {e, (int32_t)st, (int32_t)(ln < 0 ? 0 : ln), nit > 1 ? slots++ : -1});
-      }
-    }
-    X.n_gitems[sd] = (int64_t)items.size() / 4;
-    X.n_gcomb[sd] = (int64_t)comb.size() / 4;
-    X.n_gslots[sd] = slots;
-    FIA_HIP_TRY(X.gitems[sd].reserve(sizeof(int32_t) * items.size()));
-    FIA_HIP_TRY(hipMemcpy(X.gitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
-    if (!comb.empty()) {
-      FIA_HIP_TRY(X.gcomb[sd].reserve(sizeof(int32_t) * comb.size()));
-      FIA_HIP_TRY(hipMemcpy(X.gcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
-    }
+    X.hord[sd] = ord;
   }
+  FIA_HIP_TRY(build_gram_lists(c, gram_chunk(kGramChunk)));
   keys_sorted.release();
   tmp.release();
   // pair set, load factor <= 1/2
@@ -410,7 +428,7 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
 }
 
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_items, hipStream_t s) {
+                        int64_t max_items, int qb, hipStream_t s) {
   const int64_t U = c->idx.U, I = c->idx.I, nE = U + I;
   FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
   FIA_HIP_TRY(c->gstart.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
@@ -433,11 +451,11 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
   const int64_t nt = (Q > nE + 1 ? Q : nE + 1);
   hipLaunchKernelGGL(k_group_fill, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr, U, I,
                      c->gstart.as<int64_t>(), c->grank.as<int32_t>(), c->gcnt.as<unsigned long long>(),
-                     c->gq.as<int32_t>(), c->wcnt.as<int64_t>());
+                     c->gq.as<int32_t>(), c->wcnt.as<int64_t>(), qb);
   FIA_HIP_TRY(hipGetLastError());
   FIA_HIP_TRY(exclusive_scan_i64(c, c->wcnt.as<int64_t>(), c->wstart.as<int64_t>(), nE + 1, s));
   hipLaunchKernelGGL(k_item_fill, dim3(grid_for(max_items, 256, 16384)), dim3(256), 0, s, c->wstart.as<int64_t>(),
-                     c->gcnt.as<unsigned long long>(), nE, c->witems.as<int32_t>());
+                     c->gcnt.as<unsigned long long>(), nE, c->witems.as<int32_t>(), qb);
   return hipGetLastError();
 }
 

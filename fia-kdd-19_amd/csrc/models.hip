@@ -1797,6 +1797,15 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
     }
   }
   constexpr int GSP = (GS + 1) & ~1;
+  // Gram slice length: short slices for parallelism, long enough that the partial Grams
+  // of split lists (GSP doubles each) stay a few bytes per rating (MI355X: ml-1m-ex MF k=16
+  // best at 256, 20M MF k=64 loses 30% at 256 vs 512)
+  {
+    int64_t want = M::ncf ? 512 : 256;
+    while (!M::ncf && want < 4096 && want < GSP) want *= 2;
+    want = gram_chunk(want);
+    if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want));
+  }
   const Index& X = c->idx;
   for (int sd = 0; sd < 2; ++sd)
     if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
@@ -1861,7 +1870,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int64_t max_items = max_chunks;
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s));
-  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, s));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, kQueryBlock, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks; the
