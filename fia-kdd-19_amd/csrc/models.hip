@@ -1708,6 +1708,181 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// MF entity-shared scoring with the work item's 256 ratings as 4 rows per lane and the
+// embedding walked 8 coordinates at a time: each 16-B LDS broadcast of a query's x feeds
+// 8 FMAs (4 rows x 2), where k_score_grouped's one row per lane at k >= 64 spent one LDS
+// read per FMA.  Same arithmetic order (and bits) as k_score_grouped; one candidate
+// slot set per work item (spc = 1).
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
+    QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
+    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(!M::ncf && M::K % 8 == 0, "MF, k a multiple of 8");
+  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 8;
+  constexpr int RSW = (4 + M::SB + 1) & ~1;      // staged record words, even: 16-B aligned x chunks
+  constexpr int NSV = (K + 1 + 63) / 64;
+  __shared__ double srec[kScoreThreads / 64][QB * RSW];
+  __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_items = wstart[nE];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
+    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int sd = g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(g - A.U) : g;
+    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
+    const int64_t gn = gstart[g + 1] - gb;
+    const int nq = gn < QB ? (int)gn : QB;
+    const int32_t* __restrict__ oth = A.other[sd] + lb;
+    const float* __restrict__ rat = A.rating[sd] + lb;
+    const int32_t* __restrict__ rw = A.row[sd] + lb;
+    double selfv[NSV];
+#pragma unroll
+    for (int v = 0; v < NSV; ++v) {
+      const int c = v * 64 + lane;
+      const float* Es = sd == 0 ? A.t[0] : A.t[1];
+      const float* Bs = sd == 0 ? A.t[2] : A.t[3];
+      selfv[v] = c < K ? (double)Es[(int64_t)e * K + c] : (double)Bs[e];
+    }
+#define SV(c) readlane_d(selfv[(c) / 64], (c) % 64)
+    double* __restrict__ rl = srec[wave];
+    int64_t* __restrict__ bl = sbase[wave];
+    __builtin_amdgcn_wave_barrier();
+    for (int t = lane; t < QB * RSW; t += 64) {
+      const int j = t / RSW, c = t - j * RSW;
+      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
+      rl[t] = c < 4 + M::SB ? rec[(int64_t)q * M::R + (c < 4 ? c : 4 + sd * M::SB + (c - 4))] : 0.0;
+    }
+    if (lane < QB) {
+      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
+      const int64_t* qb = qbase + 4 * (int64_t)q;
+      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
+      bl[QB + lane] = qb[2 + sd] + cidx;
+      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;
+    }
+    int32_t o_[RT], row_[RT];
+    float y_[RT], gb_[RT];
+    bool ok_[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int idx = r * 64 + lane;
+      ok_[r] = idx < len;
+      const int li = ok_[r] ? idx : 0;
+      o_[r] = oth[li];
+      y_[r] = rat[li];
+      row_[r] = rw[li];
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
+    const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
+    const float* __restrict__ bt = sd == 0 ? A.t[3] : A.t[2];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) gb_[r] = bt[o_[r]];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double ea[RT], acc[QB][RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      ea[r] = 0.0;
+#pragma unroll
+      for (int j = 0; j < QB; ++j) acc[j][r] = 0.0;
+    }
+#pragma unroll 1
+    for (int c0 = 0; c0 < K; c0 += CK) {
+      float ga[RT][CK];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + c0);
+        const float4 a = src[0], b = src[1];
+        ga[r][0] = a.x; ga[r][1] = a.y; ga[r][2] = a.z; ga[r][3] = a.w;
+        ga[r][4] = b.x; ga[r][5] = b.y; ga[r][6] = b.z; ga[r][7] = b.w;
+      }
+#pragma unroll
+      for (int cc = 0; cc < CK; ++cc) {
+        const double sc = SV(c0 + cc);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) ea[r] = fma(sc, (double)ga[r][cc], ea[r]);
+      }
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        if (j >= nq) break;
+        const double2* __restrict__ xr = reinterpret_cast<const double2*>(rl + j * RSW + 4 + K + c0);
+#pragma unroll
+        for (int c2 = 0; c2 < CK / 2; ++c2) {
+          const double2 x2 = xr[c2];
+#pragma unroll
+          for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.x, (double)ga[r][2 * c2], acc[j][r]);
+#pragma unroll
+          for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.y, (double)ga[r][2 * c2 + 1], acc[j][r]);
+        }
+      }
+    }
+    {
+      const double gbias = (double)A.t[4][0];
+      const double bself = SV(K);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) ea[r] = ea[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
+    }
+#undef SV
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      if (j >= nq) break;
+      const double* __restrict__ Rj = rl + j * RSW;
+      const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
+      const double xsb = Rj[4 + 2 * K + 1], dup_o = Rj[4 + 2 * K + 2];
+      const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
+      double la[RT], lv[RT];
+      int lp[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        double ee = ea[r], ss = acc[j][r] + xsb;
+        if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
+        const double infl = (2.0 * ee * ss + cq) * inv_n;
+        const int idx = r * 64 + lane;
+        if (ok_[r]) {
+          if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
+          if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+        }
+        lp[r] = ok_[r] ? cidx * kChunk + idx : -1;
+        la[r] = ok_[r] ? topk_key(infl) : -2.0;
+        lv[r] = infl;
+      }
+      if (K_top > 0) {
+        double pa = INFINITY;
+        int pp = -1;
+        for (int t = 0; t < K_top; ++t) {
+          double ba = -2.0, bv = 0.0;
+          int bp = 0x7fffffff;
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
+              ba = la[r]; bp = lp[r]; bv = lv[r];
+            }
+          wave_best(ba, bp, bv);
+          if (lane == 0) {
+            const bool okk = ba > -1.5;
+            const int64_t slot = cbj * K_top + t;
+            cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+            cand_val[slot] = okk ? bv : NAN;
+          }
+          pa = ba;
+          pp = bp;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // Merge the chunk candidates of every query (one wave per query).
 __global__ __launch_bounds__(64) void k_topk_merge(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi,
                                                    int64_t Q, const int64_t* __restrict__ coff, int K, int spc,
@@ -1858,7 +2033,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // costs more than the shared gathers save (ml-1m-ex 36.6 vs 39.3 M q/s).
   const bool grouped = c->score_mode >= 0 ? c->score_mode == 1 : (M::ncf || M::K >= 32);
   // candidate slot sets per chunk: k_score_grouped writes one per pass
-  const int spc = grouped ? kScoreRows / score_rw<M>() : 1;
+  constexpr bool grouped_mf = !M::ncf && M::K >= 32;        // k_score_grouped_mf (k >= 32: measured faster)
+  const int spc = grouped && !grouped_mf ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));
   if (K > 0) {
     FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc)));
@@ -1900,10 +2076,16 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   if (grid > 8192) grid = 8192;
   phase_begin(c, 2, s);
   if (grouped) {
-    hipLaunchKernelGGL(k_score_grouped<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
-                       c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
-                       c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
-                       c->cand_val.as<double>());
+    if constexpr (grouped_mf)
+      hipLaunchKernelGGL(k_score_grouped_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                         c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                         c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                         c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+    else
+      hipLaunchKernelGGL(k_score_grouped<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                         c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
+                         c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
+                         c->cand_val.as<double>());
   } else {
     if constexpr (!M::ncf) {
       hipLaunchKernelGGL(k_score_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q,
