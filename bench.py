@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="answer only this rank's 1/S share of the query set (contiguous, balanced by n_q): "
                          "with S=8 at N=1 this is one GPU's share of the 8-GPU strong-scaling job")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one captured HIP graph (measured no faster on MI355X)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
@@ -71,6 +73,16 @@ def load_data(cfg):
     k = cfg["k"]
     params = (synth.mf_params if cfg["model"] == "MF" else synth.ncf_params)(d["U"], d["I"], k, 0)
     return d, params
+
+
+def score_kernel(cfg):
+    """The library's scoring kernel for this config (models.hip / bigk.hip schedule choice)."""
+    k, model = cfg["k"], cfg["model"]
+    if k >= 128 or (model == "NCF" and k >= 64):
+        return "k_big_score"
+    if model == "NCF":
+        return "k_score_grouped"
+    return "k_score_mf" if k <= 16 else "k_score_grouped_mf"
 
 
 def bytes_per_query(model, k, n):
@@ -190,7 +202,7 @@ def main():
     # the top-K exchange: one async all_gather per step, overlapped with the next step
     tg = TopKGather(all_sizes, K, dev) if world > 1 else None
 
-    def step():
+    def compute():
         if big_k:
             ctx.prepare_for(qu, qi)    # caches for this GPU's users/items only (fia_prepare_for)
         else:
@@ -199,6 +211,9 @@ def main():
             ctx.count_related(qb_u, qb_i, off_b, want_total=False)
             ctx.query_batch(qb_u, qb_i, off_b, tot_b, rel, infl, xbuf, K, tp[b0 * K:b1 * K],
                             tix[b0 * K:b1 * K], tv[b0 * K:b1 * K])
+
+    def step():
+        compute()
         if tg is not None:
             tg.start(tix.view(Q, K), tv.view(Q, K))
 
@@ -207,14 +222,48 @@ def main():
     if tg is not None:
         tg.wait()
     torch.cuda.synchronize(dev)
+    # per-phase breakdown (informational) from a few instrumented steps; the timed steps
+    # below record only the scoring phase's event pair (the roofline kernel time)
     ctx.profile_read()
     ctx.set_profiling(True)
+    for _ in range(min(args.steps, 5)):
+        compute()
+    torch.cuda.synchronize(dev)
+    ctx.set_profiling(False)
+    phases = ctx.profile_read()
+    # the timed steps: the whole step (prepare + related counts + query batches) captured
+    # once as a HIP graph and replayed -- every kernel still runs every step; the graph only
+    # removes host launch cost and inter-kernel gaps.  fia_prepare_for (large k) decides
+    # the cache size on the host, so those configs run eagerly.
+    use_graph = args.graph and not big_k
+    graph = None
+    if use_graph:
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            compute()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            compute()
+        torch.cuda.synchronize(dev)
+
+    def timed_step():
+        if graph is not None:
+            graph.replay()
+        else:
+            compute()
+        if tg is not None:
+            tg.start(tix.view(Q, K), tv.view(Q, K))
+
+    ctx.set_profiling(True, phases=("score",))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        timed_step()
     if tg is not None:
         tg.wait()
     torch.cuda.synchronize(dev)
@@ -222,7 +271,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_profiling(False)
-    phases = ctx.profile_read()
+    timed = ctx.profile_read()          # scoring kernel duration over the timed region
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -230,14 +279,14 @@ def main():
 
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * Q * args.steps / elapsed
-    score_ms = phases["score"][0] / max(phases["score"][1], 1)          # per launch
+    score_ms = timed["score"][0] / max(timed["score"][1], 1)            # per launch, timed region
     bytes_launch = float(bytes_per_query(cfg["model"], k, n_q).sum()) / len(batches)   # mean per launch
     achieved = bytes_launch / (score_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config:
+            if tj.get("config") == args.config and tj.get("kernel", "").startswith(score_kernel(cfg)):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -252,11 +301,11 @@ def main():
                 "real held-out test pairs; synthetic parameters",
         "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_gpu": Q,
                    "n_train": int(tu.size), "related_ratings_per_gpu_step": int(total), "topk": K,
-                   "query_batches": len(batches), "shard_of": args.shard_of,
+                   "query_batches": len(batches), "shard_of": args.shard_of, "hip_graph": use_graph,
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_score", "kernel_ms": score_ms, "algorithmic_bytes_per_launch": bytes_launch},
+                     "kernel": score_kernel(cfg), "kernel_ms": score_ms, "algorithmic_bytes_per_launch": bytes_launch},
         "phases_ms_per_step": {p: (v[0] / max(v[1], 1)) for p, v in phases.items()},
         "index_build_s": index_s,
     }

@@ -19,7 +19,7 @@ static bool pooled_event(fia_ctx* c, hipEvent_t* e) {
 }
 
 void phase_begin(fia_ctx* c, int phase, hipStream_t s) {
-  if (!c->profiling) return;
+  if (!(c->profiling >> phase & 1u)) return;
   hipEvent_t a, b;
   if (!pooled_event(c, &a)) return;
   if (!pooled_event(c, &b)) { c->events.pool.push_back(a); return; }
@@ -28,7 +28,7 @@ void phase_begin(fia_ctx* c, int phase, hipStream_t s) {
 }
 
 void phase_end(fia_ctx* c, int phase, hipStream_t s) {
-  if (!c->profiling || c->events.ev[phase].empty()) return;
+  if (!(c->profiling >> phase & 1u) || c->events.ev[phase].empty()) return;
   (void)hipEventRecord(c->events.ev[phase].back().second, s);
 }
 
@@ -302,9 +302,9 @@ int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
   })
 }
 
-int fia_set_profiling(fia_ctx* c, int enable) {
+int fia_set_profiling(fia_ctx* c, int phase_mask) {
   if (!c) return FIA_ERR_INVALID;
-  c->profiling = enable != 0;
+  c->profiling = (unsigned)phase_mask & ((1u << FIA_NUM_PHASES) - 1u);
   return FIA_OK;
 }
 

@@ -187,7 +187,7 @@ struct fia_ctx {
   fia::DevBuf lscr;       // double LDL^T factor scratch, one slab per resident solve workgroup
   int num_cus = 0;
   int score_mode = -1;    // scoring schedule: -1 auto, 0 per-query chunks, 1 entity-shared (FIA_SCORE)
-  bool profiling = false;
+  unsigned profiling = 0;   // bit p: record phase p (fia_set_profiling)
   fia::PhaseEvents events;
 };
 

@@ -157,8 +157,12 @@ class Context(object):
         self._check(rc, "fia_query_batch")
 
     # ---- profiling ----
-    def set_profiling(self, on):
-        self._check(self.lib.fia_set_profiling(self.h, 1 if on else 0), "fia_set_profiling")
+    def set_profiling(self, on, phases=None):
+        """on: record HIP-event pairs for the phases named in `phases` (all if None)."""
+        mask = 0
+        if on:
+            mask = 0x1f if phases is None else sum(1 << PHASES.index(p) for p in phases)
+        self._check(self.lib.fia_set_profiling(self.h, mask), "fia_set_profiling")
 
     def profile_read(self):
         ms = (ctypes.c_double * FIA_NUM_PHASES)()

@@ -135,13 +135,16 @@ int fia_query_batch(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, co
 int fia_num_params(const fia_ctx* ctx);
 
 /* Phase timing with HIP events recorded on the call's stream (for the
- * roofline figures of bench.py).  While enabled every fia_prepare /
- * fia_query_batch records one event pair per phase; fia_profile_read
- * synchronises them, returns per-phase sums (ms) and counts, and clears them.
+ * roofline figures of bench.py).  phase_mask bit p enables phase p (0 = off,
+ * FIA_PROFILE_ALL = every phase): every fia_prepare / fia_query_batch then
+ * records one event pair per enabled phase; fia_profile_read synchronises
+ * them, returns per-phase sums (ms) and counts, and clears them.
  * Phases: 0 prepare, 1 solve, 2 score (the dominant gather/scoring kernel),
- * 3 topk merge, 4 chunk build + scan. */
+ * 3 topk merge, 4 chunk build + scan.  Each pair costs a little stream time,
+ * so timed runs enable only the phase they price. */
 #define FIA_NUM_PHASES 5
-int fia_set_profiling(fia_ctx* ctx, int enable);
+#define FIA_PROFILE_ALL 0x1f
+int fia_set_profiling(fia_ctx* ctx, int phase_mask);
 int fia_profile_read(fia_ctx* ctx, double* ms_sum /*[FIA_NUM_PHASES]*/, int64_t* counts /*[FIA_NUM_PHASES]*/);
 
 #ifdef __cplusplus

@@ -1,0 +1,35 @@
+"""HBM traffic per dispatch of one kernel from two rocprofv3 PMC passes
+(FETCH_SIZE and WRITE_SIZE, separate runs) -> profiles/score_traffic.json.
+
+    python tools/traffic_json.py <config> <kernel-substring> <fetch_dir> <write_dir> <out.json>
+
+MI355X_MICROARCH.md: FETCH_SIZE (KB) reports half the bytes of a wide coalesced read
+on gfx950 -> doubled; WRITE_SIZE (KB) taken as is."""
+import csv
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter, kernel):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    cfg, kern, fdir, wdir, out = sys.argv[1:6]
+    f, nf = per_dispatch(fdir, "FETCH_SIZE", kern)
+    w, nw = per_dispatch(wdir, "WRITE_SIZE", kern)
+    res = {"config": cfg, "kernel": kern, "hbm_bytes_per_launch": (2 * f + w) * 1024.0,
+           "fetch_bytes_per_launch": 2 * f * 1024.0, "write_bytes_per_launch": w * 1024.0,
+           "dispatches": [nf, nw],
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 5); "
+                     "FETCH_SIZE(KB) x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE(KB), x1024, "
+                     "per-dispatch average"}
+    json.dump(res, open(out, "w"), indent=2)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
