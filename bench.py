@@ -81,7 +81,7 @@ def score_kernel(cfg):
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_big_score"
     if model == "NCF":
-        return "k_score_grouped"
+        return "k_score_ncf"
     return "k_score_mf" if k <= 16 else "k_score_grouped_mf"
 
 

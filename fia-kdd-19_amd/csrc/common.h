@@ -172,7 +172,9 @@ struct fia_ctx {
   fia::DevBuf self[2];    // int32 [N] entity owning list position p of side s
   uint64_t self_version = ~0ull;
   fia::DevBuf resid;      // double [N]   e_j = r-hat_j - y_j by train row
+                          //   (small-k NCF: [2][N] by list position of each side)
   fia::DevBuf gm[2];      // double [N*k] NCF g_mlp = W1_side . d1_j by train row, per side
+                          //   (small-k NCF: [k][N] by list position)
   fia::DevBuf slot[2];    // int32 [n_entity] Gram cache slot (-1 = not cached) after fia_prepare_for
   fia::DevBuf mark;       // uint8 [U + I] entities referenced by the fia_prepare_for queries
   bool subset = false;    // caches cover only the fia_prepare_for entities (large-k models)

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "common.h"
 
@@ -48,7 +49,7 @@ struct NCFm {
   static constexpr int H2 = K / 2;
   static constexpr int Ds = 2 * K;
   static constexpr int D = 2 * Ds;
-  static constexpr int SB = 4 * K + 1;          // per-side record: tself, yv, bx, ag, dup_other
+  static constexpr int SB = 2 * K + 1;          // per-side record: x_mlp, W3g * x_gmf, dup_other
   static constexpr int R = 4 + 2 * SB;          // header: inv_n, c_q, x.v, r-hat(u,i)
   static constexpr bool ncf = true;
   __device__ static bool decayed(int) { return true; }
@@ -158,70 +159,6 @@ struct NCFWeights {   // LDS copies (fp64)
   double W3[3 * (K / 2)];   // [W3m (k/2) ; W3g (k)]
 };
 
-// d1 = ((W2 * (W3m . 1[z2>0])) . 1[z1>0]); returns W3m . relu(z2)
-template <int K>
-__device__ __forceinline__ double ncf_mlp(const NCFWeights<K>& w, const double (&z1)[K], double (&d1)[K]) {
-  constexpr int H = K / 2;
-  double z2[H];
-#pragma unroll
-  for (int d = 0; d < H; ++d) z2[d] = w.b2[d];
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    double h = z1[c] > 0.0 ? z1[c] : 0.0;
-#pragma unroll
-    for (int d = 0; d < H; ++d) z2[d] = fma(w.W2[c * H + d], h, z2[d]);
-  }
-  double mlp = 0.0, d2[H];
-#pragma unroll
-  for (int d = 0; d < H; ++d) {
-    bool on = z2[d] > 0.0;
-    mlp = fma(w.W3[d], on ? z2[d] : 0.0, mlp);
-    d2[d] = on ? w.W3[d] : 0.0;
-  }
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    double t = 0.0;
-#pragma unroll
-    for (int d = 0; d < H; ++d) t = fma(w.W2[c * H + d], d2[d], t);
-    d1[c] = z1[c] > 0.0 ? t : 0.0;
-  }
-  return mlp;
-}
-
-// Same MLP, but instead of materialising d1 returns yv . d1 (the scoring kernel's only
-// use of it), one hidden unit at a time: 1.5k live doubles fewer per row.
-template <int K>
-__device__ __forceinline__ double ncf_mlp_dot(const NCFWeights<K>& w, const double (&z1)[K],
-                                              const double* __restrict__ yv, double& yd1) {
-  constexpr int H = K / 2;
-  double z2[H];
-#pragma unroll
-  for (int d = 0; d < H; ++d) z2[d] = w.b2[d];
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    const double h = z1[c] > 0.0 ? z1[c] : 0.0;
-#pragma unroll
-    for (int d = 0; d < H; ++d) z2[d] = fma(w.W2[c * H + d], h, z2[d]);
-  }
-  double mlp = 0.0;
-#pragma unroll
-  for (int d = 0; d < H; ++d) {
-    const bool on = z2[d] > 0.0;
-    mlp = fma(w.W3[d], on ? z2[d] : 0.0, mlp);
-    z2[d] = on ? w.W3[d] : 0.0;                 // z2 now holds d2
-  }
-  double acc = 0.0;
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    double t = 0.0;
-#pragma unroll
-    for (int d = 0; d < H; ++d) t = fma(w.W2[c * H + d], z2[d], t);
-    if (z1[c] > 0.0) acc = fma(yv[c], t, acc);
-  }
-  yd1 = acc;
-  return mlp;
-}
-
 template <int K>
 __device__ void load_ncf_weights(NCFWeights<K>& w, const float* W2, const float* b2, const float* W3) {
   constexpr int H = K / 2;
@@ -245,105 +182,6 @@ __global__ void k_ncf_l1(const float* __restrict__ emb, const float* __restrict_
 #pragma unroll
   for (int a = 0; a < K; ++a) acc = fma((double)x[a], (double)W1[(row_off + a) * K + c], acc);
   out[t] = acc;
-}
-
-// ------------------------------------------------------------------------------------
-// Entity Gram: gram[e] = sum over e's rating list of g g^T (packed lower, Ds)
-//   MF  g = [emb_other(o) ; 1]
-//   NCF g = [W1_self^T-side d1 (k) ; W3g * gmf_other(o) (k)]
-// One workgroup per entity; ratings in tiles of TILE, g staged in LDS.
-// ------------------------------------------------------------------------------------
-template <class M>
-struct GramTile {
-  static constexpr int TILE = M::ncf ? (M::K <= 16 ? 128 : 64) : 64;
-  static constexpr int GS = M::Ds * (M::Ds + 1) / 2;
-  static constexpr int MAXE = (GS + kPrepThreads - 1) / kPrepThreads;
-  static constexpr int LD = M::Ds + 1;   // padded row
-};
-
-template <class M>
-__global__ __launch_bounds__(kPrepThreads) void k_gram(
-    int side, int64_t n_ent, const int64_t* __restrict__ ptr, const int32_t* __restrict__ other,
-    const float* __restrict__ emb_other,      // MF: other side embedding; NCF: other side gmf table
-    const double* __restrict__ l1_self, const double* __restrict__ l1_other, const float* __restrict__ W1,
-    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-    const float* __restrict__ W3, double* __restrict__ gram) {
-  using GT = GramTile<M>;
-  constexpr int K = M::K, TILE = GT::TILE, LD = GT::LD, GS = GT::GS, MAXE = GT::MAXE;
-  __shared__ double g[TILE * LD];
-  __shared__ double W1s[M::ncf ? K * K : 1];     // W1 rows of this side, [a][c]
-  __shared__ double b1s[M::ncf ? K : 1];
-  __shared__ NCFWeights<M::ncf ? K : 2> w;
-  const int64_t e = blockIdx.x;
-  if (e >= n_ent) return;
-  const int tid = threadIdx.x;
-  if constexpr (M::ncf) {
-    for (int t = tid; t < K * K; t += blockDim.x) W1s[t] = W1[side * K * K + t];
-    for (int t = tid; t < K; t += blockDim.x) b1s[t] = b1[t];
-    load_ncf_weights<K>(w, W2, b2, W3);
-  }
-  int er[MAXE], ec[MAXE];
-  double acc[MAXE];
-#pragma unroll
-  for (int m = 0; m < MAXE; ++m) {
-    int idx = tid + m * kPrepThreads;
-    int r = (int)((sqrtf(8.0f * idx + 1.0f) - 1.0f) * 0.5f);
-    while (tri(r + 1, 0) <= idx) ++r;
-    while (tri(r, 0) > idx) --r;
-    er[m] = r;
-    ec[m] = idx - tri(r, 0);
-    acc[m] = 0.0;
-  }
-  const int64_t b = ptr[e], n = ptr[e + 1] - b;
-  for (int64_t t0 = 0; t0 < n; t0 += TILE) {
-    const int rows = (int)((n - t0) < TILE ? (n - t0) : TILE);
-    __syncthreads();
-    for (int t = tid; t < rows; t += blockDim.x) {
-      const int32_t o = other[b + t0 + t];
-      double* gr = g + t * LD;
-      if constexpr (!M::ncf) {
-        double row[K];
-        load_row_f32<K>(emb_other + (int64_t)o * K, row);
-#pragma unroll
-        for (int c = 0; c < K; ++c) gr[c] = row[c];
-        gr[K] = 1.0;
-      } else {
-        constexpr int H = K / 2;
-        double z1[K], d1[K];
-#pragma unroll
-        for (int c = 0; c < K; ++c) z1[c] = l1_self[e * K + c] + l1_other[(int64_t)o * K + c] + b1s[c];
-        (void)ncf_mlp<K>(w, z1, d1);
-#pragma unroll
-        for (int a = 0; a < K; ++a) {
-          double s = 0.0;
-#pragma unroll
-          for (int c = 0; c < K; ++c) s = fma(W1s[a * K + c], d1[c], s);
-          gr[a] = s;
-        }
-        double row[K];
-        load_row_f32<K>(emb_other + (int64_t)o * K, row);
-#pragma unroll
-        for (int a = 0; a < K; ++a) gr[K + a] = w.W3[H + a] * row[a];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < MAXE; ++m) {
-      if (tid + m * kPrepThreads < GS) {
-        const double* pr = g + er[m];
-        const double* pc = g + ec[m];
-        double s = acc[m];
-        for (int t = 0; t < rows; ++t) s = fma(pr[t * LD], pc[t * LD], s);
-        acc[m] = s;
-      }
-    }
-  }
-  double* out = gram + e * ((GS + 1) & ~1);
-#pragma unroll
-  for (int m = 0; m < MAXE; ++m) {
-    int idx = tid + m * kPrepThreads;
-    if (idx < GS) out[idx] = acc[m];
-  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -527,6 +365,11 @@ struct QueryArgs {
   const float* t[10];
   double wd, damping;
   PairTable pairs;
+  // NCF, per list position of each side (written by k_gram_ncf_mfma):
+  // g_mlp,j = W1_side . d1_j coordinate-major [k][N], and e_j = r-hat_j - y_j [side][N]
+  const double* lgm[2];
+  const double* lres;
+  int64_t N;
 };
 
 // One wave per query.  COLS: the two blocks of a query whose test pair is not a train row
@@ -747,25 +590,17 @@ __global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t
       S0[2 * K + 2] = (double)i;  S1[2 * K + 2] = (double)u;
     }
   } else {
+    // x . g_j = x_mlp . g_mlp,j + (W3g * x_gmf) . gmf_other(j)  (k_score_ncf)
     constexpr int H2 = K / 2;
     for (int c = lane; c < K; c += kSolveThreads) {
-      S0[c] = A.l1[0][(int64_t)u * K + c] + sb1[c];
-      S1[c] = A.l1[1][(int64_t)i * K + c] + sb1[c];
-      double y0 = 0.0, y1 = 0.0;
-      for (int a = 0; a < K; ++a) {
-        y0 = fma(v[a], sW1[a * K + c], y0);
-        y1 = fma(v[Ds + a], sW1[(K + a) * K + c], y1);
-      }
-      S0[K + c] = y0;
-      S1[K + c] = y1;
+      S0[c] = v[c];
+      S1[c] = v[Ds + c];
       const double w3g = w.W3[H2 + c];
-      S0[2 * K + c] = w3g * v[K + c];
-      S1[2 * K + c] = w3g * v[Ds + K + c];
-      S0[3 * K + c] = w3g * th[K + c];
-      S1[3 * K + c] = w3g * th[Ds + K + c];
+      S0[K + c] = w3g * v[K + c];
+      S1[K + c] = w3g * v[Ds + K + c];
     }
     if (lane == 0) {
-      S0[4 * K] = (double)i;  S1[4 * K] = (double)u;
+      S0[2 * K] = (double)i;  S1[2 * K] = (double)u;
     }
   }
   }   // work loop
@@ -997,6 +832,9 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
 // W3g * gmf_other (k)] -- to the wave's LDS tile; then C += G^T G by
 // v_mfma_f64_16x16x4_f64 over the tile's row-quads (lane l reads G[4s + l/16][16t + l%16],
 // both the A and the B operand; same map as k_gram_mf_mfma).
+// The same pass stores, per list position p, what scoring needs of the rating and
+// nothing of the query: g_mlp = W1_side . d1 to lgm[c * N + p] (coalesced per coordinate)
+// and e = r-hat - y to lres[p] (ncf:130-145), so k_score_ncf runs no MLP at all.
 // ------------------------------------------------------------------------------------
 template <class M>
 struct NCFGramCfg {
@@ -1010,7 +848,9 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
     const int32_t* __restrict__ other, const float* __restrict__ gmf_other, const double* __restrict__ l1_self,
     const double* __restrict__ l1_other, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ W3,
-    double* __restrict__ gram, double* __restrict__ part) {
+    double* __restrict__ gram, double* __restrict__ part, const float* __restrict__ gmf_self,
+    const float* __restrict__ rating, const float* __restrict__ b3, int64_t N, double* __restrict__ lgm,
+    double* __restrict__ lres) {
   constexpr int K = M::K, H = K / 2, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   constexpr int NT = Ds / 16, NP = NT * (NT + 1) / 2;
   constexpr int WAVES = NCFGramCfg<M>::WAVES, LDG = NCFGramCfg<M>::LDG;
@@ -1029,9 +869,12 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
   double* __restrict__ G = gl[wave];
   for (int64_t it = (int64_t)blockIdx.x * WAVES + wave; it < n_items; it += (int64_t)gridDim.x * WAVES) {
     const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], slot = items[4 * it + 3];
-    const int32_t* ids = other + ptr[e] + start;
-    // the entity's own layer-1 half + b1, spread over lanes
+    const int64_t lb = ptr[e] + start;
+    const int32_t* ids = other + lb;
+    // the entity's own layer-1 half + b1 and gmf row, spread over lanes
     const double selfv = lane < K ? l1_self[(int64_t)e * K + lane] + (double)b1[lane] : 0.0;
+    const double selfg = lane < K ? (double)gmf_self[(int64_t)e * K + lane] : 0.0;
+    const double bias3 = (double)b3[0];
     d4_t acc[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
@@ -1052,8 +895,13 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
 #pragma unroll
         for (int d = 0; d < H; ++d) z2[d] = fma(w.W2[c * H + d], h, z2[d]);
       }
+      double mlp = 0.0;
 #pragma unroll
-      for (int d = 0; d < H; ++d) z2[d] = z2[d] > 0.0 ? w.W3[d] : 0.0;   // d2
+      for (int d = 0; d < H; ++d) {
+        const bool on = z2[d] > 0.0;
+        mlp = fma(w.W3[d], on ? z2[d] : 0.0, mlp);
+        z2[d] = on ? w.W3[d] : 0.0;                  // d2
+      }
       double d1[K];
 #pragma unroll
       for (int c = 0; c < K; ++c) {
@@ -1063,14 +911,20 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
         d1[c] = (mask >> c) & 1 ? t : 0.0;
       }
       double* gr = G + lane * LDG;
+      const int64_t p = lb + t0 + lane;
+      double gmf = 0.0;
 #pragma unroll
       for (int a = 0; a < K; ++a) {
         double s = 0.0;
 #pragma unroll
         for (int c = 0; c < K; ++c) s = fma(W1s[a * K + c], d1[c], s);
+        const double go = (double)Go[a];
+        gmf = fma(w3g[a] * readlane_d(selfg, a), go, gmf);
         gr[a] = valid ? s : 0.0;
-        gr[K + a] = valid ? w3g[a] * (double)Go[a] : 0.0;
+        gr[K + a] = valid ? w3g[a] * go : 0.0;
+        if (valid) lgm[(int64_t)a * N + p] = s;
       }
+      if (valid) lres[p] = mlp + gmf + bias3 - (double)rating[p];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1129,186 +983,15 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
 }
 
 // ------------------------------------------------------------------------------------
-// Scoring (the dominant, HBM-streaming kernel): one WAVE per chunk of <= 64*RW
-// consecutive ratings of one side of one query; the 4 waves of a block are
-// independent (no block barrier after the NCF weight load).  Everything the chunk
-// needs from its query is wave-uniform (scalar loads).  Per rating j:
+// Scoring (the dominant, HBM-streaming kernel), MF per-query chunks: one WAVE per chunk
+// of <= kChunk consecutive ratings of one side of one query.  Per rating j:
 //   influence_j = (2 e_j s_j + c_q) / n,  s_j = x . g_j,  e_j = r-hat_j - y_j
-// (mf:240-246: x . grad L_j / n with grad L_j = 2 e_j g_j + wd * M * theta_t).
-// The chunk's K best (|influence| desc, position asc) go to its candidate slots.
-// ------------------------------------------------------------------------------------
-template <class M>
-__global__ __launch_bounds__(kScoreThreads) void k_score(
-    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
-    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  constexpr int K = M::K;
-  constexpr int RT = kScoreRows;                 // rows per lane per chunk
-  constexpr int RW = M::ncf ? 4 : kScoreRows;    // rows per lane per pass (NCF: register budget)
-  constexpr int NPASS = RT / RW;
-  __shared__ NCFWeights<M::ncf ? K : 2> w;
-  if constexpr (M::ncf) {
-    load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
-    __syncthreads();
-  }
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nchunks = coff[Q];
-  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  for (int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; ch < nchunks; ch += stride) {
-    const ChunkDesc d = cdesc[ch];
-    const int sd = d.side;
-    const int32_t* __restrict__ oth = A.other[sd] + d.list_base;
-    const float* __restrict__ rat = A.rating[sd] + d.list_base;
-    const int32_t* __restrict__ rw = A.row[sd] + d.list_base;
-    // the query record, spread over the lanes (lane c holds word c of this side's
-    // record; read back with v_readlane), loaded together with the list entries
-    const double* __restrict__ R = rec + (int64_t)d.q * M::R;
-    const double* __restrict__ Sg = R + 4 + sd * M::SB;
-    constexpr int NV = (M::SB + 63) / 64;
-    const double hv = R[lane & 3];
-    double rv[NV];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) rv[v] = Sg[v * 64 + lane < M::SB ? v * 64 + lane : M::SB - 1];
-    double ca[RT], cv[RT];
-    int cp[RT];
-#pragma unroll
-    for (int h = 0; h < NPASS; ++h) {
-      // list entries (coalesced, branch-free: lanes past the chunk end re-read entry 0),
-      // then every row's gather issued before any arithmetic
-      int32_t o_[RW], row_[RW];
-      float y_[RW];
-      bool ok_[RW];
-  #pragma unroll
-      for (int r = 0; r < RW; ++r) {
-        const int idx = (h * RW + r) * 64 + lane;
-        ok_[r] = idx < d.len;
-        const int li = ok_[r] ? idx : 0;
-        o_[r] = oth[li];
-        y_[r] = rat[li];
-        row_[r] = rw[li];
-      }
-      // pin the list loads here: without this hipcc sinks the row-index load into the
-      // (conditional) rel_idx store and serialises one HBM round trip per row
-  #pragma unroll
-      for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
-      float4 g4_[M::ncf ? 1 : RW][M::ncf ? 1 : K / 4];
-      float gb_[RW];
-      if constexpr (!M::ncf) {
-        const float* T = sd == 0 ? A.t[1] : A.t[0];
-        const float* bt = sd == 0 ? A.t[3] : A.t[2];
-  #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
-  #pragma unroll
-          for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
-          gb_[r] = bt[o_[r]];
-        }
-        // all gathers in flight before the first use
-  #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-  #pragma unroll
-          for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
-          asm volatile("" ::"v"(gb_[r]));
-        }
-      }
-      const double inv_n = readlane_d(hv, 0), cq = readlane_d(hv, 1), xv = readlane_d(hv, 2),
-                   rhat_ui = readlane_d(hv, 3);
-      const double* __restrict__ S = Sg;   // NCF reads its (longer) record directly
-      // MF: the two dot products of every row with the record's (p_self, x_self); the
-      // coordinate loop is outermost so each record word is broadcast once per chunk
-      double dot_a[RW], dot_x[RW];
-      if constexpr (!M::ncf) {
-  #define RS(c) readlane_d(rv[(c) / 64], (c) % 64)
-  #pragma unroll
-        for (int r = 0; r < RW; ++r) dot_a[r] = dot_x[r] = 0.0;
-  #pragma unroll
-        for (int c4 = 0; c4 < K / 4; ++c4) {
-  #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            const double ac = RS(4 * c4 + cc), xc = RS(K + 4 * c4 + cc);
-  #pragma unroll
-            for (int r = 0; r < RW; ++r) {
-              const float4 t = g4_[r][c4];
-              const double tv = (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w);
-              dot_a[r] = fma(ac, tv, dot_a[r]);
-              dot_x[r] = fma(xc, tv, dot_x[r]);
-            }
-          }
-        }
-      }
-      const double bias_s = M::ncf ? 0.0 : RS(2 * K), xsb = M::ncf ? 0.0 : RS(2 * K + 1);
-      const double dup_o = M::ncf ? 0.0 : RS(2 * K + 2);
-  #undef RS
-  #pragma unroll
-      for (int r = 0; r < RW; ++r) {
-        const int32_t o = o_[r];
-        const double y = (double)y_[r];
-        double e, s;
-        if constexpr (!M::ncf) {
-          e = dot_a[r] + bias_s + (double)gb_[r] - y;
-          s = dot_x[r] + xsb;
-          if ((double)o == dup_o) { e = rhat_ui - y; s = xv; }
-        } else {
-          const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o * K;
-          const float* G = (sd == 0 ? A.t[3] : A.t[2]) + (int64_t)o * K;   // other side gmf row
-          double z1[K];
-  #pragma unroll
-          for (int c = 0; c < K; ++c) z1[c] = S[c] + L1o[c];
-          double yd1;
-          const double mlp = ncf_mlp_dot<K>(w, z1, S + K, yd1);   // yd1 = yv . d1
-          double gmf = 0.0;
-          s = yd1;
-  #pragma unroll
-          for (int c = 0; c < K; ++c) {
-            const double g = (double)G[c];
-            s = fma(S[2 * K + c], g, s);
-            gmf = fma(S[3 * K + c], g, gmf);
-          }
-          e = mlp + gmf + (double)A.t[9][0] - y;
-          if ((double)o == S[4 * K]) { e = rhat_ui - y; s = xv; }
-        }
-        const double infl = (2.0 * e * s + cq) * inv_n;
-        const int idx = (h * RW + r) * 64 + lane;
-        if (ok_[r]) {   // streaming outputs: nontemporal, so they do not evict the gathered tables from L2
-          if (influence) __builtin_nontemporal_store(infl, influence + d.out_base + idx);
-          if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + d.out_base + idx);
-        }
-        cp[h * RW + r] = ok_[r] ? d.pos0 + idx : -1;
-        ca[h * RW + r] = ok_[r] ? topk_key(infl) : -2.0;
-        cv[h * RW + r] = infl;
-      }
-    }
-    if (K_top > 0) {
-      double pa = INFINITY;
-      int pp = -1;
-      for (int t = 0; t < K_top; ++t) {
-        double ba = -2.0, bv = 0.0;
-        int bp = 0x7fffffff;
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
-            ba = ca[r]; bp = cp[r]; bv = cv[r];
-          }
-        wave_best(ba, bp, bv);
-        if (lane == 0) {
-          const bool ok = ba > -1.5;
-          cand_pos[ch * K_top + t] = ok ? bp : -1;
-          cand_val[ch * K_top + t] = ok ? bv : NAN;
-        }
-        pa = ba;
-        pp = bp;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// MF per-query-chunk scoring, software-pipelined across the wave's chunks.  A chunk's
-// critical path is three dependent round trips (descriptor -> list entries + record ->
-// gathered rows); here the next chunk's descriptor, list entries and record words are
-// loaded while the current chunk's gathers are in flight, so each chunk waits on one
-// round trip.  Same arithmetic (and bits) as k_score.
+// (mf:240-246: x . grad L_j / n with grad L_j = 2 e_j g_j + wd * M * theta_t); the
+// chunk's K best (|influence| desc, position asc) go to its candidate slots.
+// Software-pipelined across the wave's chunks: a chunk's critical path is three
+// dependent round trips (descriptor -> list entries + record -> gathered rows); the next
+// chunk's descriptor, list entries and record words are loaded while the current
+// chunk's gathers are in flight, so each chunk waits on one round trip.
 // ------------------------------------------------------------------------------------
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_mf(
@@ -1448,9 +1131,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf(
 // Entity-shared scoring.  A work item is one chunk (<= kChunk ratings) of ONE entity's
 // list (user list R_u or item list C_i) together with every query of the batch that
 // has that entity.  The list entries, the gathered other-side embedding rows and the
-// per-rating residual e_j = r-hat_j - y_j (and, for NCF, the MLP backward vector
-// d1_j) depend on the train rating only, so they are loaded / computed once per work
-// item and reused for every query in the group; per query only s_jq = x_q . g_j is
+// per-rating residual e_j = r-hat_j - y_j depend on the train rating only, so they are
+// loaded / computed once per work item and reused for every query in the group; per query only s_jq = x_q . g_j is
 // new.  influence_jq = (2 e_j s_jq + c_q) / n_q  (mf:240-246).  The test pair's own
 // train row takes e and s from the query record (bit-identical copies, see k_solve).
 // ------------------------------------------------------------------------------------
@@ -1458,7 +1140,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf(
 // vectors); kScoreRows / score_rw passes per work item, one candidate slot set each
 template <class M>
 constexpr int score_rw() {
-  return M::ncf ? (M::K >= 32 ? 1 : 2) : (M::K >= 64 ? 1 : M::K >= 32 ? 2 : 4);
+  return M::K >= 64 ? 1 : M::K >= 32 ? 2 : 4;
 }
 
 template <class M>
@@ -1467,6 +1149,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(!M::ncf, "MF scoring (NCF: k_score_ncf)");
   constexpr int K = M::K;
   constexpr int RT = kScoreRows;                 // rows per lane per work item
   constexpr int RW = score_rw<M>();              // rows per lane per pass
@@ -1474,15 +1157,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
   constexpr int NSV = (K + 1 + 63) / 64;         // entity words per lane
   constexpr int QB = kQueryBlock;
   constexpr int RSW = 4 + M::SB;                  // staged record words: header + this side's block
-  __shared__ NCFWeights<M::ncf ? K : 2> w;
   // per wave: the query block's records (uniform-address reads = LDS broadcasts) and
   // per query {output base, candidate-slot base, position offset}
   __shared__ double srec[kScoreThreads / 64][QB * RSW];
   __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
-  if constexpr (M::ncf) {
-    load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
-    __syncthreads();
-  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_items = wstart[nE];
@@ -1500,19 +1178,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
     const int32_t* __restrict__ oth = A.other[sd] + lb;
     const float* __restrict__ rat = A.rating[sd] + lb;
     const int32_t* __restrict__ rw = A.row[sd] + lb;
-    // the entity's own parameters, spread over lanes (MF: embedding + bias; NCF: its
-    // layer-1 half + b1)
+    // the entity's own embedding + bias, spread over lanes
     double selfv[NSV];
 #pragma unroll
     for (int v = 0; v < NSV; ++v) {
       const int c = v * 64 + lane;
-      if constexpr (!M::ncf) {
-        const float* Es = sd == 0 ? A.t[0] : A.t[1];
-        const float* Bs = sd == 0 ? A.t[2] : A.t[3];
-        selfv[v] = c < K ? (double)Es[(int64_t)e * K + c] : (double)Bs[e];
-      } else {
-        selfv[v] = c < K ? A.l1[sd][(int64_t)e * K + c] + (double)A.t[5][c] : 0.0;
-      }
+      const float* Es = sd == 0 ? A.t[0] : A.t[1];
+      const float* Bs = sd == 0 ? A.t[2] : A.t[3];
+      selfv[v] = c < K ? (double)Es[(int64_t)e * K + c] : (double)Bs[e];
     }
 #define SV(c) readlane_d(selfv[(c) / 64], (c) % 64)
     // stage the query block (queries past the group end repeat the last one; never used)
@@ -1551,65 +1224,40 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
 #pragma unroll
       for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
       // per-rating quantities shared by the whole query block
-      float4 g4_[RW][(K + 3) / 4];               // other-side embedding row (MF: dot with x; NCF: gmf row)
+      float4 g4_[RW][(K + 3) / 4];               // other-side embedding row
       double ej[RW];                             // residual r-hat_j - y_j
-      double d1_[M::ncf ? RW : 1][M::ncf ? K : 1];   // NCF: masked backward vector
       {
-        const float* T = sd == 0 ? (M::ncf ? A.t[3] : A.t[1]) : (M::ncf ? A.t[2] : A.t[0]);
+        const float* T = sd == 0 ? A.t[1] : A.t[0];
         float gb_[RW];
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
           const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
 #pragma unroll
           for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
-          if constexpr (!M::ncf) gb_[r] = (sd == 0 ? A.t[3] : A.t[2])[o_[r]];
+          gb_[r] = (sd == 0 ? A.t[3] : A.t[2])[o_[r]];
         }
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
 #pragma unroll
           for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
         }
-        if constexpr (!M::ncf) {
-          const double gbias = (double)A.t[4][0];
-          const double bself = SV(K);
+        const double gbias = (double)A.t[4][0];
+        const double bself = SV(K);
 #pragma unroll
-          for (int r = 0; r < RW; ++r) ej[r] = 0.0;
+        for (int r = 0; r < RW; ++r) ej[r] = 0.0;
 #pragma unroll
-          for (int c4 = 0; c4 < K / 4; ++c4)
+        for (int c4 = 0; c4 < K / 4; ++c4)
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-              const double pc = SV(4 * c4 + cc);
+          for (int cc = 0; cc < 4; ++cc) {
+            const double pc = SV(4 * c4 + cc);
 #pragma unroll
-              for (int r = 0; r < RW; ++r) {
-                const float4 t = g4_[r][c4];
-                ej[r] = fma(pc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), ej[r]);
-              }
-            }
-#pragma unroll
-          for (int r = 0; r < RW; ++r) ej[r] = ej[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
-        } else {
-          const double b3 = (double)A.t[9][0];
-          const float* Gs = (sd == 0 ? A.t[2] : A.t[3]) + (int64_t)e * K;   // own gmf row
-          const float* W3g = A.t[8] + K / 2;
-#pragma unroll
-          for (int r = 0; r < RW; ++r) {
-            const double* L1o = A.l1[sd == 0 ? 1 : 0] + (int64_t)o_[r] * K;
-            double z1[K];
-#pragma unroll
-            for (int c = 0; c < K; ++c) z1[c] = SV(c) + L1o[c];
-            const double mlp = ncf_mlp<K>(w, z1, d1_[r]);
-            double gmf = 0.0;
-#pragma unroll
-            for (int c4 = 0; c4 < K / 4; ++c4) {
+            for (int r = 0; r < RW; ++r) {
               const float4 t = g4_[r][c4];
-              gmf = fma((double)W3g[4 * c4 + 0] * (double)Gs[4 * c4 + 0], (double)t.x, gmf);
-              gmf = fma((double)W3g[4 * c4 + 1] * (double)Gs[4 * c4 + 1], (double)t.y, gmf);
-              gmf = fma((double)W3g[4 * c4 + 2] * (double)Gs[4 * c4 + 2], (double)t.z, gmf);
-              gmf = fma((double)W3g[4 * c4 + 3] * (double)Gs[4 * c4 + 3], (double)t.w, gmf);
+              ej[r] = fma(pc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), ej[r]);
             }
-            ej[r] = mlp + gmf + b3 - (double)y_[r];
           }
-        }
+#pragma unroll
+        for (int r = 0; r < RW; ++r) ej[r] = ej[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
       }
       // every query of the block: s_jq = x_q . g_j, then influence, outputs, candidates
 #pragma unroll 1
@@ -1619,47 +1267,23 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
         const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
         const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
         double sj[RW];
-        double dup_o;
-        if constexpr (!M::ncf) {
 #pragma unroll
-          for (int r = 0; r < RW; ++r) sj[r] = 0.0;
+        for (int r = 0; r < RW; ++r) sj[r] = 0.0;
 #pragma unroll
-          for (int c4 = 0; c4 < K / 4; ++c4)
+        for (int c4 = 0; c4 < K / 4; ++c4)
 #pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-              const double xc = RS(K + 4 * c4 + cc);
+          for (int cc = 0; cc < 4; ++cc) {
+            const double xc = RS(K + 4 * c4 + cc);
 #pragma unroll
-              for (int r = 0; r < RW; ++r) {
-                const float4 t = g4_[r][c4];
-                sj[r] = fma(xc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), sj[r]);
-              }
+            for (int r = 0; r < RW; ++r) {
+              const float4 t = g4_[r][c4];
+              sj[r] = fma(xc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), sj[r]);
             }
-          const double xsb = RS(2 * K + 1);
-#pragma unroll
-          for (int r = 0; r < RW; ++r) sj[r] += xsb;
-          dup_o = RS(2 * K + 2);
-        } else {
-#pragma unroll
-          for (int r = 0; r < RW; ++r) sj[r] = 0.0;
-#pragma unroll
-          for (int c = 0; c < K; ++c) {
-            const double yc = RS(K + c);
-#pragma unroll
-            for (int r = 0; r < RW; ++r) sj[r] = fma(yc, d1_[r][c], sj[r]);
           }
+        const double xsb = RS(2 * K + 1);
 #pragma unroll
-          for (int c4 = 0; c4 < K / 4; ++c4)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-              const double bc = RS(2 * K + 4 * c4 + cc);
-#pragma unroll
-              for (int r = 0; r < RW; ++r) {
-                const float4 t = g4_[r][c4];
-                sj[r] = fma(bc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), sj[r]);
-              }
-            }
-          dup_o = RS(4 * K);
-        }
+        for (int r = 0; r < RW; ++r) sj[r] += xsb;
+        const double dup_o = RS(2 * K + 2);
 #undef RS
         double la[RW], lv[RW];
         int lp[RW];
@@ -1883,6 +1507,176 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// NCF entity-shared scoring.  Same work items, query blocks and outputs as
+// k_score_grouped_mf, but nothing of the MLP is recomputed here: per list position the
+// Gram pass stored g_mlp,j = W1_side . d1_j (coordinate-major, so every load below is a
+// coalesced 512-B wave row) and e_j, and the solve stored x_mlp and W3g * x_gmf, so
+//   s_jq = x_mlp,q . g_mlp,j + (W3g * x_gmf,q) . gmf_other(j)      (ncf:193-280)
+// is 2k FMAs per (rating, query) over the work item's 256 ratings (4 rows per lane).
+// One candidate slot set per work item (spc = 1).
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
+    QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
+    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(M::ncf && M::K % 4 == 0, "NCF, k a multiple of 4");
+  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4;
+  constexpr int RSW = (4 + M::SB + 1) & ~1;      // staged record words, even: 16-B aligned x chunks
+  __shared__ __attribute__((aligned(16))) double srec[kScoreThreads / 64][QB * RSW];
+  __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t n_items = wstart[nE];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  const int64_t N = A.N;
+  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
+    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int sd = g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(g - A.U) : g;
+    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
+    const int64_t gn = gstart[g + 1] - gb;
+    const int nq = gn < QB ? (int)gn : QB;
+    const int32_t* __restrict__ oth = A.other[sd] + lb;
+    const float* __restrict__ rat = A.rating[sd] + lb;
+    const int32_t* __restrict__ rw = A.row[sd] + lb;
+    const double* __restrict__ gml = A.lgm[sd] + lb;
+    const double* __restrict__ res = A.lres + (int64_t)sd * N + lb;
+    double* __restrict__ rl = srec[wave];
+    int64_t* __restrict__ bl = sbase[wave];
+    __builtin_amdgcn_wave_barrier();
+    for (int t = lane; t < QB * RSW; t += 64) {
+      const int j = t / RSW, c = t - j * RSW;
+      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
+      rl[t] = c < 4 + M::SB ? rec[(int64_t)q * M::R + (c < 4 ? c : 4 + sd * M::SB + (c - 4))] : 0.0;
+    }
+    if (lane < QB) {
+      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
+      const int64_t* qb = qbase + 4 * (int64_t)q;
+      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
+      bl[QB + lane] = qb[2 + sd] + cidx;
+      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
+    }
+    int32_t o_[RT], row_[RT], li_[RT];
+    float y_[RT];
+    double ej[RT];
+    bool ok_[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int idx = r * 64 + lane;
+      ok_[r] = idx < len;
+      li_[r] = ok_[r] ? idx : 0;
+      o_[r] = oth[li_[r]];
+      y_[r] = rat[li_[r]];
+      row_[r] = rw[li_[r]];
+      ej[r] = res[li_[r]];
+    }
+    const float* __restrict__ T = sd == 0 ? A.t[3] : A.t[2];    // other side's gmf table
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // NQ = nq rounded up to a power of two: a static query count per path, so the
+    // accumulators stay in registers without per-query exits (the padding columns
+    // score copies of the last query and are never written out)
+    auto run = [&](auto nq_c) {
+      constexpr int NQ = decltype(nq_c)::value;
+      double acc[NQ][RT];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j)
+#pragma unroll
+        for (int r = 0; r < RT; ++r) acc[j][r] = 0.0;
+#pragma unroll 1
+      for (int c0 = 0; c0 < K; c0 += CK) {
+        double gm_[RT][CK];
+        float go_[RT][CK];
+        // scalar base per coordinate + 32-bit lane offsets (kept opaque so the compiler
+        // does not strength-reduce them into 2 VGPRs per (row, coordinate) pointer)
+        const double* gbase = gml + (int64_t)c0 * N;
+        asm volatile("" : "+s"(gbase));
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+#pragma unroll
+          for (int cc = 0; cc < CK; ++cc) gm_[r][cc] = gbase[(int64_t)cc * N + li_[r]];
+          const float4 t = *reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + c0);
+          go_[r][0] = t.x; go_[r][1] = t.y; go_[r][2] = t.z; go_[r][3] = t.w;
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+          const double2* __restrict__ xm = reinterpret_cast<const double2*>(rl + j * RSW + 4 + c0);
+          const double2* __restrict__ xg = reinterpret_cast<const double2*>(rl + j * RSW + 4 + K + c0);
+#pragma unroll
+          for (int c2 = 0; c2 < CK / 2; ++c2) {
+            const double2 a = xm[c2], b = xg[c2];
+#pragma unroll
+            for (int r = 0; r < RT; ++r) {
+              acc[j][r] = fma(a.x, gm_[r][2 * c2], acc[j][r]);
+              acc[j][r] = fma(a.y, gm_[r][2 * c2 + 1], acc[j][r]);
+              acc[j][r] = fma(b.x, (double)go_[r][2 * c2], acc[j][r]);
+              acc[j][r] = fma(b.y, (double)go_[r][2 * c2 + 1], acc[j][r]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        if (j >= nq) continue;   // padding columns (copies of the last query)
+        const double* __restrict__ Rj = rl + j * RSW;
+        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
+        const double dup_o = Rj[4 + 2 * K];
+        const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
+        double la[RT], lv[RT];
+        int lp[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          double ee = ej[r], ss = acc[j][r];
+          if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
+          const double infl = (2.0 * ee * ss + cq) * inv_n;
+          const int idx = r * 64 + lane;
+          if (ok_[r]) {
+            if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
+            if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+          }
+          lp[r] = ok_[r] ? cidx * kChunk + idx : -1;
+          la[r] = ok_[r] ? topk_key(infl) : -2.0;
+          lv[r] = infl;
+        }
+        if (K_top > 0) {
+          double pa = INFINITY;
+          int pp = -1;
+          for (int t = 0; t < K_top; ++t) {
+            double ba = -2.0, bv = 0.0;
+            int bp = 0x7fffffff;
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+              if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
+                ba = la[r]; bp = lp[r]; bv = lv[r];
+              }
+            wave_best(ba, bp, bv);
+            if (lane == 0) {
+              const bool okk = ba > -1.5;
+              const int64_t slot = cbj * K_top + t;
+              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+              cand_val[slot] = okk ? bv : NAN;
+            }
+            pa = ba;
+            pp = bp;
+          }
+        }
+      }
+    };
+    if (nq <= 1) run(std::integral_constant<int, 1>{});
+    else if (nq <= 2) run(std::integral_constant<int, 2>{});
+    else if (nq <= 4) run(std::integral_constant<int, 4>{});
+    else run(std::integral_constant<int, QB>{});
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // Merge the chunk candidates of every query (one wave per query).
 __global__ __launch_bounds__(64) void k_topk_merge(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi,
                                                    int64_t Q, const int64_t* __restrict__ coff, int K, int spc,
@@ -1947,6 +1741,10 @@ QueryArgs make_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
   A.pairs.cnt = c->idx.pcnt.as<int32_t>();
   A.pairs.sum = c->idx.psum.as<double>();
   A.pairs.mask = (unsigned long long)(c->idx.pcap - 1);
+  A.lgm[0] = c->gm[0].as<double>();
+  A.lgm[1] = c->gm[1].as<double>();
+  A.lres = c->resid.as<double>();
+  A.N = c->idx.N;
   return A;
 }
 
@@ -1985,6 +1783,9 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   for (int sd = 0; sd < 2; ++sd)
     if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
   if constexpr (M::ncf) {
+    const int64_t N = X.N;
+    for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1)));
+    FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * N + 1)));
     for (int sd = 0; sd < 2; ++sd) {
       if (n_ent[sd] == 0 || X.n_gitems[sd] == 0) continue;
       constexpr int WAVES = NCFGramCfg<M>::WAVES;
@@ -1994,7 +1795,8 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
                          X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
                          c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4],
                          c->p.t[5], c->p.t[6], c->p.t[7], c->p.t[8], c->gram[sd].as<double>(),
-                         c->gpart[sd].as<double>());
+                         c->gpart[sd].as<double>(), c->p.t[sd == 0 ? 2 : 3], X.side[sd].rating.as<float>(),
+                         c->p.t[9], N, c->gm[sd].as<double>(), c->resid.as<double>() + sd * N);
       FIA_HIP_TRY(hipGetLastError());
     }
   } else {
@@ -2028,13 +1830,13 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                       int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
   // Auto schedule (measured on MI355X, profiles/): entity-shared scoring wins whenever
-  // the per-rating work is larger than a 64-B gather (NCF's MLP, k >= 32) -- yelp-ex NCF
-  // 15.8 vs 13.3 M q/s, 20M MF k=64 855 vs 429 k q/s; for MF k <= 16 the group build
-  // costs more than the shared gathers save (ml-1m-ex 36.6 vs 39.3 M q/s).
-  const bool grouped = c->score_mode >= 0 ? c->score_mode == 1 : (M::ncf || M::K >= 32);
+  // the per-rating work is larger than a 64-B gather (k >= 32) -- 20M MF k=64 855 vs
+  // 429 k q/s; for MF k <= 16 the group build costs more than the shared gathers save
+  // (ml-1m-ex 36.6 vs 39.3 M q/s).  NCF scoring is entity-shared only (k_score_ncf).
+  const bool grouped = M::ncf || (c->score_mode >= 0 ? c->score_mode == 1 : M::K >= 32);
   // candidate slot sets per chunk: k_score_grouped writes one per pass
-  constexpr bool grouped_mf = !M::ncf && M::K >= 32;        // k_score_grouped_mf (k >= 32: measured faster)
-  const int spc = grouped && !grouped_mf ? kScoreRows / score_rw<M>() : 1;
+  constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
+  const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));
   if (K > 0) {
     FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc)));
@@ -2076,7 +1878,12 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   if (grid > 8192) grid = 8192;
   phase_begin(c, 2, s);
   if (grouped) {
-    if constexpr (grouped_mf)
+    if constexpr (M::ncf)
+      hipLaunchKernelGGL(k_score_ncf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                         c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                         c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                         c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+    else if constexpr (one_pass)
       hipLaunchKernelGGL(k_score_grouped_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
                          c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
                          c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
@@ -2087,15 +1894,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
                          c->cand_val.as<double>());
   } else {
-    if constexpr (!M::ncf) {
+    if constexpr (!M::ncf)
       hipLaunchKernelGGL(k_score_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q,
                          c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence,
                          K, c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-    } else {
-      hipLaunchKernelGGL(k_score<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(),
-                         c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence, K,
-                         c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-    }
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);
