@@ -278,25 +278,44 @@ __device__ void ldlt_cols(double* __restrict__ Hb, double* __restrict__ vb) {
 }
 
 // Register-resident solve of the two blocks of a query (N = Ds <= 64): lane c holds column c
-// of the symmetric block (all N rows), fully unrolled right-looking LDL^T whose pivot
-// column is broadcast lane j -> all (v_readlane; with 2N <= 64 both blocks run at once in
-// the two 32-lane halves and the broadcast is a 32-wide shuffle).  After step j lane c > j
-// keeps L[c][j] in col[j] (forward solve) and its own column below the diagonal holds
-// d_c L[r][c] (backward solve).  g: right-hand sides [2N] (LDS), v: solutions [2N] (LDS).
+// of the symmetric block (all N rows) and runs a fully unrolled right-looking LDL^T; with
+// 2N <= 64 both blocks run at once in the two 32-lane halves.  Step j needs the pivot
+// column A[r][j], r >= j -- by symmetry lane r's own col[j] -- in every lane: each lane
+// publishes col[j] to an LDS slot (one ds_write per lane) and the column comes back as
+// uniform-address reads (LDS broadcasts, two rows per ds_read_b128), consumed right away
+// by the rank-1 update.  (A v_readlane / ds_bpermute per element costs N^2/2 serialised
+// broadcasts: NCF k=16 spent 0.84 ms of 0.95 there.)  After step j lane c > j keeps
+// L[c][j] in col[j] (forward solve) and its own column below the diagonal holds
+// d_c L[r][c] (backward solve); the two triangular solves broadcast one value per step
+// by v_readlane.  g: right-hand sides [2N] (LDS), v: solutions [2N] (LDS),
+// P: pivot-column staging [64] (LDS).
 template <int N>
 __device__ __forceinline__ double bcast_col(double x, int j) {
-  if constexpr (2 * N <= 64) return __shfl(x, j, 32);
-  else return readlane_d(x, j);
+  if constexpr (2 * N <= 64) {
+    const double lo = readlane_d(x, j), hi = readlane_d(x, 32 + j);
+    return (threadIdx.x & 32) ? hi : lo;
+  } else {
+    return readlane_d(x, j);
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <class M>
 __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* __restrict__ Gi, double s2n,
                                   double wd, double damping, const double* __restrict__ g, double* __restrict__ v,
-                                  double* __restrict__ Hs) {
+                                  double* __restrict__ Hs, double* __restrict__ P) {
   constexpr int N = M::Ds, GS = N * (N + 1) / 2;
   static_assert(N <= 64, "one column per lane");
   constexpr bool PAR = 2 * N <= 64;
-  const int lane = threadIdx.x;
+  // lane-derived values are made opaque where they are used, so the compiler does not
+  // hoist N column addresses and N lane masks out of the caller's query loop (spills)
+  int lane = threadIdx.x;
+  asm volatile("" : "+v"(lane));
   // both cached blocks into LDS with coalesced loads; the per-lane column reads below are
   // strided (A[r][c] for r < c sits in row c of the packed lower layout)
   for (int t = lane; t < GS; t += kSolveThreads) {
@@ -310,6 +329,7 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
     const int c = PAR ? lane & 31 : lane;
     const bool live = c < N;
     const double* __restrict__ Gb = Hs + b * GS;
+    double* __restrict__ Pb = P + b * 32;     // 64 slots: every lane publishes unconditionally
     double col[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) {
@@ -323,23 +343,33 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
     double dinv_own = 0.0;
 #pragma unroll
     for (int j = 0; j < N; ++j) {
-      const double ij = 1.0 / bcast_col<N>(col[j], j);
+      Pb[c] = col[j];                           // A[c][j] (= col[j] by symmetry); rows >= j read
+      wave_lds_sync();
+      const double ij = 1.0 / Pb[j];
       if (c == j) dinv_own = ij;
       const double f = c > j ? col[j] * ij : 0.0;
+      // fixed trip count: the inner loop unrolls before the outer one, so a j-dependent
+      // bound would leave col[] indexed at run time (scratch)
 #pragma unroll
-      for (int r = j + 1; r < N; ++r) col[r] = fma(-bcast_col<N>(col[r], j), f, col[r]);
+      for (int r = 0; r < N; ++r)
+        if (r > j) col[r] = fma(-Pb[r], f, col[r]);
       if (c > j) col[j] = f;
+      wave_lds_sync();                          // this step's reads before the next writes
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) {             // L y = g
+      int ci = c;
+      asm volatile("" : "+v"(ci));
       const double yi = bcast_col<N>(y, i);
-      if (c > i) y = fma(-col[i], yi, y);
+      if (ci > i) y = fma(-col[i], yi, y);
     }
     y *= dinv_own;
 #pragma unroll
     for (int j = N - 1; j >= 0; --j) {        // L^T x = D^-1 y
+      int cj = c;
+      asm volatile("" : "+v"(cj));
       const double xj = bcast_col<N>(y, j);
-      if (c < j) y = fma(-col[j] * dinv_own, xj, y);
+      if (cj < j) y = fma(-col[j] * dinv_own, xj, y);
     }
     if (live) v[b * N + c] = y;
   }
@@ -383,7 +413,7 @@ __global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t
                                                          int32_t* __restrict__ coupled_out) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
   __shared__ double H[COLS ? 2 * GS : D * (D + 1) / 2];
-  __shared__ double v[D], g[D], th[D], dd[D], ww[D];
+  __shared__ double v[D], g[D], th[D], dd[D], ww[D], pv[64];
   __shared__ double sh[4 * K + 8];
   // NCF weights staged once per block (fp64), read by every query the block solves
   __shared__ NCFWeights<M::ncf ? K : 2> w;
@@ -500,7 +530,7 @@ __global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t
       continue;
     }
     if constexpr (M::Ds <= 64) {
-      solve_blocks_regs<M>(Gu, Gi, s2n, A.wd, A.damping, g, v, H);
+      solve_blocks_regs<M>(Gu, Gi, s2n, A.wd, A.damping, g, v, H, pv);
     } else {
       // block b: H_b = (2/n) Gram_b + wd on decayed coordinates + damping, column-major
       for (int t = lane; t < 2 * GS; t += kSolveThreads) {
