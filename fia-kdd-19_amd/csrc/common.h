@@ -146,6 +146,7 @@ struct fia_ctx {
   // NCF: per-entity layer-1 halves Pm*W1[:k] and Qm*W1[k:] (fp64) [U*k], [I*k]
   fia::DevBuf l1[2];
   fia::DevBuf gpart[2];   // partial Grams of long lists (fp64, [n_gslots * GSP])
+  fia::DevBuf wf64;       // NCF weights in fp64 [W2 | b2 | W3 | W1 | b1] (scalar-cache reads)
   bool prepared = false;
   // per-batch scratch
   fia::DevBuf rec;        // per-query scoring record (fp64)

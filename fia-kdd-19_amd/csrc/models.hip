@@ -856,6 +856,34 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
 }
 
 // ------------------------------------------------------------------------------------
+// NCF weights in fp64, laid out for uniform reads: a kernel indexing them with
+// compile-time offsets gets them through the scalar cache into SGPRs (one SGPR-pair
+// operand per v_fma_f64) instead of LDS broadcasts that the scheduler hoists into VGPRs.
+// ------------------------------------------------------------------------------------
+template <int K>
+struct NCFW64 {
+  static constexpr int H = K / 2;
+  static constexpr int W2 = 0, B2 = W2 + K * H, W3 = B2 + H, W1 = W3 + 3 * H, B1 = W1 + 2 * K * K;
+  static constexpr int SIZE = B1 + K;
+};
+
+template <int K>
+__global__ void k_ncf_weights_f64(const float* __restrict__ W1, const float* __restrict__ b1,
+                                  const float* __restrict__ W2, const float* __restrict__ b2,
+                                  const float* __restrict__ W3, double* __restrict__ out) {
+  using L = NCFW64<K>;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < L::SIZE; t += gridDim.x * blockDim.x) {
+    float x;
+    if (t < L::B2) x = W2[t];
+    else if (t < L::W3) x = b2[t - L::B2];
+    else if (t < L::W1) x = W3[t - L::W3];
+    else if (t < L::B1) x = W1[t - L::W1];
+    else x = b1[t - L::B1];
+    out[t] = (double)x;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // NCF Gram on the f64 matrix cores.  A wave takes one work item (<= kGramChunk ratings
 // of one entity's list) in rounds of 64 ratings: lane l runs rating l's MLP forward and
 // backward (TF ReluGrad masks) and writes its g row -- [W1_side . d1 (k) ;
@@ -876,25 +904,17 @@ template <class M>
 __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
     int side, int64_t n_items, const int32_t* __restrict__ items, const int64_t* __restrict__ ptr,
     const int32_t* __restrict__ other, const float* __restrict__ gmf_other, const double* __restrict__ l1_self,
-    const double* __restrict__ l1_other, const float* __restrict__ W1, const float* __restrict__ b1,
-    const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ W3,
-    double* __restrict__ gram, double* __restrict__ part, const float* __restrict__ gmf_self,
-    const float* __restrict__ rating, const float* __restrict__ b3, int64_t N, double* __restrict__ lgm,
-    double* __restrict__ lres) {
+    const double* __restrict__ l1_other, const double* __restrict__ wd, double* __restrict__ gram,
+    double* __restrict__ part, const float* __restrict__ gmf_self, const float* __restrict__ rating,
+    const float* __restrict__ b3, int64_t N, double* __restrict__ lgm, double* __restrict__ lres) {
   constexpr int K = M::K, H = K / 2, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   constexpr int NT = Ds / 16, NP = NT * (NT + 1) / 2;
   constexpr int WAVES = NCFGramCfg<M>::WAVES, LDG = NCFGramCfg<M>::LDG;
+  using L = NCFW64<K>;
   static_assert(M::ncf && Ds % 16 == 0 && K <= 64, "NCF Gram tiling");
-  __shared__ NCFWeights<K> w;
-  __shared__ double W1s[K * K];     // this side's half of W1, [a][c]
-  __shared__ double w3g[K];
   __shared__ double gl[WAVES][64 * LDG];
-  for (int t = threadIdx.x; t < K * K; t += blockDim.x) W1s[t] = (double)W1[side * K * K + t];
-  for (int t = threadIdx.x; t < K; t += blockDim.x) w3g[t] = (double)W3[H + t];
-  load_ncf_weights<K>(w, W2, b2, W3);
-  __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, grp = lane >> 4;
   double* __restrict__ G = gl[wave];
   for (int64_t it = (int64_t)blockIdx.x * WAVES + wave; it < n_items; it += (int64_t)gridDim.x * WAVES) {
@@ -902,20 +922,28 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
     const int64_t lb = ptr[e] + start;
     const int32_t* ids = other + lb;
     // the entity's own layer-1 half + b1 and gmf row, spread over lanes
-    const double selfv = lane < K ? l1_self[(int64_t)e * K + lane] + (double)b1[lane] : 0.0;
+    const double selfv = lane < K ? l1_self[(int64_t)e * K + lane] + wd[L::B1 + lane] : 0.0;
     const double selfg = lane < K ? (double)gmf_self[(int64_t)e * K + lane] : 0.0;
     const double bias3 = (double)b3[0];
     d4_t acc[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
     for (int t0 = 0; t0 < len; t0 += 64) {
+      // weight pointers re-formed every round through an opaque offset: hoisted out of the
+      // loop, the ~k^2 scalar loads would be kept in SGPRs and spilled
+      int z0 = 0;
+      asm volatile("" : "+s"(z0));
+      const double* __restrict__ W2 = wd + z0 + L::W2;
+      const double* __restrict__ B2 = wd + z0 + L::B2;
+      const double* __restrict__ W3 = wd + z0 + L::W3;
+      const double* __restrict__ W1s = wd + z0 + L::W1 + side * K * K;   // this side's half of W1, [a][c]
       const bool valid = t0 + lane < len;
       const int32_t o = ids[valid ? t0 + lane : 0];
       const double* L1o = l1_other + (int64_t)o * K;
       const float* Go = gmf_other + (int64_t)o * K;
       double z2[H];
 #pragma unroll
-      for (int d = 0; d < H; ++d) z2[d] = w.b2[d];
+      for (int d = 0; d < H; ++d) z2[d] = B2[d];
       uint64_t mask = 0;
 #pragma unroll
       for (int c = 0; c < K; ++c) {
@@ -923,25 +951,28 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
         mask |= (uint64_t)(z > 0.0) << c;
         const double h = z > 0.0 ? z : 0.0;
 #pragma unroll
-        for (int d = 0; d < H; ++d) z2[d] = fma(w.W2[c * H + d], h, z2[d]);
+        for (int d = 0; d < H; ++d) z2[d] = fma(W2[c * H + d], h, z2[d]);
+        __builtin_amdgcn_sched_barrier(0);   // weight loads stay next to their use (SGPRs)
       }
       double mlp = 0.0;
 #pragma unroll
       for (int d = 0; d < H; ++d) {
         const bool on = z2[d] > 0.0;
-        mlp = fma(w.W3[d], on ? z2[d] : 0.0, mlp);
-        z2[d] = on ? w.W3[d] : 0.0;                  // d2
+        mlp = fma(W3[d], on ? z2[d] : 0.0, mlp);
+        z2[d] = on ? W3[d] : 0.0;                    // d2
       }
       double d1[K];
 #pragma unroll
       for (int c = 0; c < K; ++c) {
         double t = 0.0;
 #pragma unroll
-        for (int d = 0; d < H; ++d) t = fma(w.W2[c * H + d], z2[d], t);
+        for (int d = 0; d < H; ++d) t = fma(W2[c * H + d], z2[d], t);
         d1[c] = (mask >> c) & 1 ? t : 0.0;
+        __builtin_amdgcn_sched_barrier(0);
       }
       double* gr = G + lane * LDG;
-      const int64_t p = lb + t0 + lane;
+      // per-round uniform base; the lane offset is added last
+      double* lg = lgm + (lb + t0);
       double gmf = 0.0;
 #pragma unroll
       for (int a = 0; a < K; ++a) {
@@ -949,12 +980,14 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
 #pragma unroll
         for (int c = 0; c < K; ++c) s = fma(W1s[a * K + c], d1[c], s);
         const double go = (double)Go[a];
-        gmf = fma(w3g[a] * readlane_d(selfg, a), go, gmf);
+        const double w3g = W3[H + a];
+        gmf = fma(w3g * readlane_d(selfg, a), go, gmf);
         gr[a] = valid ? s : 0.0;
-        gr[K + a] = valid ? w3g[a] * go : 0.0;
-        if (valid) lgm[(int64_t)a * N + p] = s;
+        gr[K + a] = valid ? w3g * go : 0.0;
+        if (valid) (lg + (int64_t)a * N)[lane] = s;
+        __builtin_amdgcn_sched_barrier(0);
       }
-      if (valid) lres[p] = mlp + gmf + bias3 - (double)rating[p];
+      if (valid) lres[lb + t0 + lane] = mlp + gmf + bias3 - (double)rating[lb + t0 + lane];
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1816,6 +1849,10 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
     const int64_t N = X.N;
     for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1)));
     FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * N + 1)));
+    FIA_HIP_TRY(c->wf64.reserve(sizeof(double) * NCFW64<K>::SIZE));
+    hipLaunchKernelGGL(k_ncf_weights_f64<K>, dim3(1), dim3(256), 0, s, c->p.t[4], c->p.t[5], c->p.t[6], c->p.t[7],
+                       c->p.t[8], c->wf64.as<double>());
+    FIA_HIP_TRY(hipGetLastError());
     for (int sd = 0; sd < 2; ++sd) {
       if (n_ent[sd] == 0 || X.n_gitems[sd] == 0) continue;
       constexpr int WAVES = NCFGramCfg<M>::WAVES;
@@ -1823,10 +1860,10 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
       if (grid > 16384) grid = 16384;
       hipLaunchKernelGGL(k_gram_ncf_mfma<M>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, sd, X.n_gitems[sd],
                          X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
-                         c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(), c->p.t[4],
-                         c->p.t[5], c->p.t[6], c->p.t[7], c->p.t[8], c->gram[sd].as<double>(),
-                         c->gpart[sd].as<double>(), c->p.t[sd == 0 ? 2 : 3], X.side[sd].rating.as<float>(),
-                         c->p.t[9], N, c->gm[sd].as<double>(), c->resid.as<double>() + sd * N);
+                         c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(),
+                         c->wf64.as<double>(), c->gram[sd].as<double>(), c->gpart[sd].as<double>(),
+                         c->p.t[sd == 0 ? 2 : 3], X.side[sd].rating.as<float>(), c->p.t[9], N,
+                         c->gm[sd].as<double>(), c->resid.as<double>() + sd * N);
       FIA_HIP_TRY(hipGetLastError());
     }
   } else {
