@@ -116,7 +116,7 @@ int fia_destroy(fia_ctx* c) {
     fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->scan_tmp,
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
                            &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->wcnt,
-                           &c->wstart, &c->witems, &c->resid,  &c->wf64,  &c->qwork,  &c->xb,       &c->syslist,
+                           &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,
                            &c->cpllist, &c->lscr, &c->mark};
     for (auto* b : bufs) b->release();
     for (auto& v : c->events.ev)

@@ -1123,17 +1123,7 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
     FIA_HIP_TRY(hipStreamSynchronize(s));
   }
   FIA_HIP_TRY(big_work_lists(c, qu ? marks : nullptr));
-  if (c->self_version != X.version) {
-    for (int sd = 0; sd < 2; ++sd) {
-      FIA_HIP_TRY(c->self[sd].reserve(sizeof(int32_t) * (size_t)(N + 1)));
-      if (N > 0) {
-        hipLaunchKernelGGL(k_self, dim3(gN), dim3(256), 0, s, N, n_ent[sd], X.side[sd].ptr.as<int64_t>(),
-                           c->self[sd].as<int32_t>());
-        FIA_HIP_TRY(hipGetLastError());
-      }
-    }
-    c->self_version = X.version;
-  }
+  FIA_HIP_TRY(ensure_self(c, s));
   FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(N + 1)));
   if constexpr (!M::ncf) {
     if (N > 0) {
@@ -1245,6 +1235,23 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
 #define FIA_BIG_CASES(X) \
   X(FIA_MODEL_MF, 128, BMF<128>) X(FIA_MODEL_MF, 256, BMF<256>) X(FIA_MODEL_NCF, 64, BNCF<64>) \
   X(FIA_MODEL_NCF, 128, BNCF<128>) X(FIA_MODEL_NCF, 256, BNCF<256>)
+
+// per-list-position owning entity of both sides (rebuilt when the index changes)
+hipError_t ensure_self(fia_ctx* c, hipStream_t s) {
+  const Index& X = c->idx;
+  if (c->self_version == X.version) return hipSuccess;
+  const int64_t N = X.N, n_ent[2] = {X.U, X.I};
+  for (int sd = 0; sd < 2; ++sd) {
+    FIA_HIP_TRY(c->self[sd].reserve(sizeof(int32_t) * (size_t)(N + 1)));
+    if (N > 0) {
+      hipLaunchKernelGGL(k_self, dim3(grid_cap((N + 255) / 256, 65536)), dim3(256), 0, s, N, n_ent[sd],
+                         X.side[sd].ptr.as<int64_t>(), c->self[sd].as<int32_t>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+  }
+  c->self_version = X.version;
+  return hipSuccess;
+}
 
 bool big_supported(int model, int k) {
 #define X(m, kk, T) if (model == m && k == kk) return true;

@@ -146,7 +146,6 @@ struct fia_ctx {
   // NCF: per-entity layer-1 halves Pm*W1[:k] and Qm*W1[k:] (fp64) [U*k], [I*k]
   fia::DevBuf l1[2];
   fia::DevBuf gpart[2];   // partial Grams of long lists (fp64, [n_gslots * GSP])
-  fia::DevBuf wf64;       // NCF weights in fp64 [W2 | b2 | W3 | W1 | b1] (scalar-cache reads)
   bool prepared = false;
   // per-batch scratch
   fia::DevBuf rec;        // per-query scoring record (fp64)
@@ -224,6 +223,7 @@ bool model_supported(int model, int k);
 
 // large-k models (bigk.hip): MF k in {128, 256}, NCF k in {64, 128, 256}
 bool big_supported(int model, int k);
+hipError_t ensure_self(fia_ctx* c, hipStream_t s);   // c->self[s]: entity of each list position
 // qu == nullptr: caches for every entity; else only for the entities of the Q queries
 hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s);
 // flag[2] |= 1 if a query's user or item has no cache after fia_prepare_for

@@ -779,6 +779,10 @@ struct GramSides {
   const float* emb_other[2];
   double* gram[2];
   double* part[2];
+  // NCF (k_gram_ncf_rows): stored g_mlp rows per side, W3, list length N
+  const double* lgm[2];
+  const float* W3;
+  int64_t N;
 };
 
 template <class M>
@@ -856,160 +860,177 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
 }
 
 // ------------------------------------------------------------------------------------
-// NCF weights in fp64, laid out for uniform reads: a kernel indexing them with
-// compile-time offsets gets them through the scalar cache into SGPRs (one SGPR-pair
-// operand per v_fma_f64) instead of LDS broadcasts that the scheduler hoists into VGPRs.
-// ------------------------------------------------------------------------------------
-template <int K>
-struct NCFW64 {
-  static constexpr int H = K / 2;
-  static constexpr int W2 = 0, B2 = W2 + K * H, W3 = B2 + H, W1 = W3 + 3 * H, B1 = W1 + 2 * K * K;
-  static constexpr int SIZE = B1 + K;
-};
-
-template <int K>
-__global__ void k_ncf_weights_f64(const float* __restrict__ W1, const float* __restrict__ b1,
-                                  const float* __restrict__ W2, const float* __restrict__ b2,
-                                  const float* __restrict__ W3, double* __restrict__ out) {
-  using L = NCFW64<K>;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < L::SIZE; t += gridDim.x * blockDim.x) {
-    float x;
-    if (t < L::B2) x = W2[t];
-    else if (t < L::W3) x = b2[t - L::B2];
-    else if (t < L::W1) x = W3[t - L::W3];
-    else if (t < L::B1) x = W1[t - L::W1];
-    else x = b1[t - L::B1];
-    out[t] = (double)x;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// NCF Gram on the f64 matrix cores.  A wave takes one work item (<= kGramChunk ratings
-// of one entity's list) in rounds of 64 ratings: lane l runs rating l's MLP forward and
-// backward (TF ReluGrad masks) and writes its g row -- [W1_side . d1 (k) ;
-// W3g * gmf_other (k)] -- to the wave's LDS tile; then C += G^T G by
-// v_mfma_f64_16x16x4_f64 over the tile's row-quads (lane l reads G[4s + l/16][16t + l%16],
-// both the A and the B operand; same map as k_gram_mf_mfma).
-// The same pass stores, per list position p, what scoring needs of the rating and
-// nothing of the query: g_mlp = W1_side . d1 to lgm[c * N + p] (coalesced per coordinate)
-// and e = r-hat - y to lres[p] (ncf:130-145), so k_score_ncf runs no MLP at all.
+// NCF per list position + entity Gram, one pass (ncf:102-145, TF ReluGrad masks).  A wave
+// takes one work item (<= gchunk positions of one entity's list, both sides in one
+// launch) in slabs of 16 positions p, e = the entity, o = other(p):
+//   z1 = (L1_self[e] + b1) + L1_other[o],  z2 = relu(z1) W2 + b2,  d2 = 1[z2 > 0] W3m,
+//   d1 = 1[z1 > 0] (W2 d2),  g_mlp = W1_side d1,  e_p = W3m.relu(z2) + W3g.(Gs_e*Go_o) + b3 - y,
+//   Gram_e += g g^T over g = [g_mlp ; W3g * Go_o]
+// and stores g_mlp to lgm[a * N + p] (coordinate-major) and e_p to lres[p] for scoring.
+// All products run on v_mfma_f64_16x16x4_f64.  The MLP runs transposed -- out^T = W . in^T
+// with the 16 positions along n -- so the weights are per-lane A operands loaded once
+// per wave and each product's C registers are the next product's B operand as they stand
+// (C register r = rows (l>>4) + 4r = the next k-slice r).  The last product runs the
+// other way round, g_mlp = d1 . W1_side^T (the same per-lane W1 values as B operand), so
+// its C register r holds positions 4r + (l>>4) x coordinates l&15 -- exactly the Gram
+// MFMA's operand for row-quad r.  No LDS, no transposes.
+// Map: lane l supplies A[l&15][l>>4] and B[l>>4][l&15]; C register r = out[(l>>4)+4r][l&15].
 // ------------------------------------------------------------------------------------
 template <class M>
-struct NCFGramCfg {
-  static constexpr int WAVES = M::K <= 16 ? 4 : 2;          // LDS: 64 rows x (2k+1) doubles per wave
-  static constexpr int LDG = 2 * M::K + 1;
-};
-
-template <class M>
-__global__ __launch_bounds__(256) void k_gram_ncf_mfma(
-    int side, int64_t n_items, const int32_t* __restrict__ items, const int64_t* __restrict__ ptr,
-    const int32_t* __restrict__ other, const float* __restrict__ gmf_other, const double* __restrict__ l1_self,
-    const double* __restrict__ l1_other, const double* __restrict__ wd, double* __restrict__ gram,
-    double* __restrict__ part, const float* __restrict__ gmf_self, const float* __restrict__ rating,
-    const float* __restrict__ b3, int64_t N, double* __restrict__ lgm, double* __restrict__ lres) {
-  constexpr int K = M::K, H = K / 2, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+__global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float* __restrict__ W1,
+                                                      const float* __restrict__ b1, const float* __restrict__ W2,
+                                                      const float* __restrict__ b2, const float* __restrict__ b3,
+                                                      const double* __restrict__ l1u, const double* __restrict__ l1i,
+                                                      const float* __restrict__ rat0, const float* __restrict__ rat1,
+                                                      double* __restrict__ lres) {
+  constexpr int K = M::K, H = K / 2, KK = K / 4, HK = (H + 3) / 4, KT = (K + 15) / 16;
+  constexpr int Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   constexpr int NT = Ds / 16, NP = NT * (NT + 1) / 2;
-  constexpr int WAVES = NCFGramCfg<M>::WAVES, LDG = NCFGramCfg<M>::LDG;
-  using L = NCFW64<K>;
-  static_assert(M::ncf && Ds % 16 == 0 && K <= 64, "NCF Gram tiling");
-  __shared__ double gl[WAVES][64 * LDG];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int col = lane & 15, grp = lane >> 4;
-  double* __restrict__ G = gl[wave];
-  for (int64_t it = (int64_t)blockIdx.x * WAVES + wave; it < n_items; it += (int64_t)gridDim.x * WAVES) {
-    const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], slot = items[4 * it + 3];
-    const int64_t lb = ptr[e] + start;
-    const int32_t* ids = other + lb;
-    // the entity's own layer-1 half + b1 and gmf row, spread over lanes
-    const double selfv = lane < K ? l1_self[(int64_t)e * K + lane] + wd[L::B1 + lane] : 0.0;
-    const double selfg = lane < K ? (double)gmf_self[(int64_t)e * K + lane] : 0.0;
-    const double bias3 = (double)b3[0];
+  static_assert(M::ncf && K % 8 == 0 && H <= 16 && Ds % 16 == 0, "NCF k in {8, 16, 32}");
+  const float* __restrict__ W3 = GSd.W3;
+  const int64_t N = GSd.N;
+  const int lane = threadIdx.x, m = lane & 15, kq = lane >> 4;
+  const int64_t n_all = GSd.n_items[0] + GSd.n_items[1];
+  // side-independent weight operands (per lane, once per wave)
+  double aW2t[KK], aW2[KT][HK], cb2[4], cw3[4], w3gk[KK], b1v[KK], w3gt[NT];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk) {
+    const int c = kq + 4 * kk;
+    aW2t[kk] = m < H ? (double)W2[c * H + m] : 0.0;           // A[h][c] = W2[c][h]
+    w3gk[kk] = (double)W3[H + c];
+    b1v[kk] = (double)b1[c];
+  }
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int row = m + 16 * t;
+#pragma unroll
+    for (int kk = 0; kk < HK; ++kk) {
+      const int h = kq + 4 * kk;
+      aW2[t][kk] = row < K && h < H ? (double)W2[row * H + h] : 0.0;          // A[c][h] = W2[c][h]
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int h = kq + 4 * r;
+    cb2[r] = h < H ? (double)b2[h] : 0.0;
+    cw3[r] = h < H ? (double)W3[h] : 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int co = 16 * t + m;
+    w3gt[t] = co >= K ? (double)W3[H + co - K] : 0.0;
+  }
+  const double bias3 = (double)b3[0];
+  int cur_side = -1;
+  double aW1[KT][KK];          // W1_side[a = m + 16t][c = kq + 4kk]: A of nothing, B of g_mlp = d1 W1^T
+  for (int64_t w = blockIdx.x; w < n_all; w += gridDim.x) {
+    const int sd = w >= GSd.n_items[0] ? 1 : 0;
+    const int64_t wi = w - (sd ? GSd.n_items[0] : 0);
+    if (sd != cur_side) {
+      cur_side = sd;
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          const int a = m + 16 * t;
+          aW1[t][kk] = a < K ? (double)W1[(int64_t)(sd * K + a) * K + kq + 4 * kk] : 0.0;
+        }
+    }
+    const int32_t* __restrict__ it = GSd.items[sd] + 4 * wi;
+    const int32_t e = it[0], start = it[1], len = it[2], slot = it[3];
+    const int64_t lb = GSd.ptr[sd][e] + start;
+    const int32_t* __restrict__ ids = GSd.other[sd] + lb;
+    const float* __restrict__ rat = (sd ? rat1 : rat0) + lb;
+    const float* __restrict__ Go = GSd.emb_other[sd];
+    const float* __restrict__ Gs = GSd.emb_other[1 - sd] + (int64_t)e * K;     // own gmf row
+    const double* __restrict__ Ls = (sd ? l1i : l1u) + (int64_t)e * K;
+    const double* __restrict__ L1o = sd ? l1u : l1i;
+    double* __restrict__ lgp = const_cast<double*>(GSd.lgm[sd]) + lb;
+    double* __restrict__ lrp = lres + (int64_t)sd * N + lb;
+    double zs[KK], gsk[KK];     // own-entity terms for this lane's coordinates
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      zs[kk] = Ls[kq + 4 * kk] + b1v[kk];
+      gsk[kk] = w3gk[kk] * (double)Gs[kq + 4 * kk];
+    }
     d4_t acc[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
-    for (int t0 = 0; t0 < len; t0 += 64) {
-      // weight pointers re-formed every round through an opaque offset: hoisted out of the
-      // loop, the ~k^2 scalar loads would be kept in SGPRs and spilled
-      int z0 = 0;
-      asm volatile("" : "+s"(z0));
-      const double* __restrict__ W2 = wd + z0 + L::W2;
-      const double* __restrict__ B2 = wd + z0 + L::B2;
-      const double* __restrict__ W3 = wd + z0 + L::W3;
-      const double* __restrict__ W1s = wd + z0 + L::W1 + side * K * K;   // this side's half of W1, [a][c]
-      const bool valid = t0 + lane < len;
-      const int32_t o = ids[valid ? t0 + lane : 0];
-      const double* L1o = l1_other + (int64_t)o * K;
-      const float* Go = gmf_other + (int64_t)o * K;
-      double z2[H];
+    for (int s0 = 0; s0 < len; s0 += 16) {
+      const bool ok = s0 + m < len;
+      const int32_t o = ids[ok ? s0 + m : 0];
+      const double* __restrict__ Lo = L1o + (int64_t)o * K;
+      double z1[KK];
 #pragma unroll
-      for (int d = 0; d < H; ++d) z2[d] = B2[d];
-      uint64_t mask = 0;
+      for (int kk = 0; kk < KK; ++kk) z1[kk] = ok ? zs[kk] + Lo[kq + 4 * kk] : 0.0;
+      d4_t z2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const double z = readlane_d(selfv, c) + L1o[c];
-        mask |= (uint64_t)(z > 0.0) << c;
-        const double h = z > 0.0 ? z : 0.0;
+      for (int kk = 0; kk < KK; ++kk)
+        z2 = __builtin_amdgcn_mfma_f64_16x16x4f64(aW2t[kk], z1[kk] > 0.0 ? z1[kk] : 0.0, z2, 0, 0, 0);
+      double mlp = 0.0, d2[4];
 #pragma unroll
-        for (int d = 0; d < H; ++d) z2[d] = fma(W2[c * H + d], h, z2[d]);
-        __builtin_amdgcn_sched_barrier(0);   // weight loads stay next to their use (SGPRs)
+      for (int r = 0; r < 4; ++r) {
+        const double z = z2[r] + cb2[r];
+        const bool on = z > 0.0;
+        mlp = fma(cw3[r], on ? z : 0.0, mlp);
+        d2[r] = on ? cw3[r] : 0.0;
       }
-      double mlp = 0.0;
+      double d1[KK];
 #pragma unroll
-      for (int d = 0; d < H; ++d) {
-        const bool on = z2[d] > 0.0;
-        mlp = fma(W3[d], on ? z2[d] : 0.0, mlp);
-        z2[d] = on ? W3[d] : 0.0;                    // d2
+      for (int t = 0; t < KT; ++t) {
+        d4_t t1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < HK; ++kk) t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(aW2[t][kk], d2[kk], t1, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * t + r < KK) d1[4 * t + r] = z1[4 * t + r] > 0.0 ? t1[r] : 0.0;
       }
-      double d1[K];
+      // g_mlp = d1 W1_side^T: C register r = positions 4r + kq, coordinates m + 16t
+      d4_t gm[KT];
 #pragma unroll
-      for (int c = 0; c < K; ++c) {
-        double t = 0.0;
+      for (int t = 0; t < KT; ++t) {
+        gm[t] = d4_t{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int d = 0; d < H; ++d) t = fma(W2[c * H + d], z2[d], t);
-        d1[c] = (mask >> c) & 1 ? t : 0.0;
-        __builtin_amdgcn_sched_barrier(0);
+        for (int kk = 0; kk < KK; ++kk) gm[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(d1[kk], aW1[t][kk], gm[t], 0, 0, 0);
       }
-      double* gr = G + lane * LDG;
-      // per-round uniform base; the lane offset is added last
-      double* lg = lgm + (lb + t0);
+      // residual of position m (mlp and the gmf dot are split over the 4 lane groups)
+      const float* __restrict__ Gom = Go + (int64_t)o * K;
       double gmf = 0.0;
 #pragma unroll
-      for (int a = 0; a < K; ++a) {
-        double s = 0.0;
+      for (int kk = 0; kk < KK; ++kk) gmf = fma(gsk[kk], (double)Gom[kq + 4 * kk], gmf);
+      double re = mlp + gmf;
+      re += __shfl_xor(re, 16);
+      re += __shfl_xor(re, 32);
+      if (kq == 0 && ok) lrp[s0 + m] = re + bias3 - (double)rat[s0 + m];
+      // Gram row-quads r: positions 4r + kq
 #pragma unroll
-        for (int c = 0; c < K; ++c) s = fma(W1s[a * K + c], d1[c], s);
-        const double go = (double)Go[a];
-        const double w3g = W3[H + a];
-        gmf = fma(w3g * readlane_d(selfg, a), go, gmf);
-        gr[a] = valid ? s : 0.0;
-        gr[K + a] = valid ? w3g * go : 0.0;
-        if (valid) (lg + (int64_t)a * N)[lane] = s;
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (valid) lres[lb + t0 + lane] = mlp + gmf + bias3 - (double)rating[lb + t0 + lane];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int nquad = (len - t0 + 3) >> 2;     // row-quads holding real ratings
-#pragma unroll 4
-      for (int sq = 0; sq < 16; ++sq) {
-        if (sq >= nquad) break;
-        double av[NT];
+      for (int r = 0; r < 4; ++r) {
+        const int pr = s0 + 4 * r + kq;
+        const bool okr = pr < len;
+        const int32_t orow = __shfl(o, 4 * r + kq);
+        double val[NT];
 #pragma unroll
-        for (int t = 0; t < NT; ++t) av[t] = G[(4 * sq + grp) * LDG + 16 * t + col];
+        for (int t = 0; t < NT; ++t) {
+          const int co = 16 * t + m;
+          const double gv = gm[t < KT ? t : KT - 1][r];
+          double x = 0.0;
+          if (co < K) {
+            x = gv;
+            if (okr) lgp[(int64_t)co * N + pr] = gv;
+          } else if (okr) {
+            x = w3gt[t] * (double)Go[(int64_t)orow * K + co - K];
+          }
+          val[t] = okr ? x : 0.0;
+        }
         int p = 0;
 #pragma unroll
         for (int ta = 0; ta < NT; ++ta)
 #pragma unroll
           for (int tb = ta; tb < NT; ++tb, ++p)
-            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ta], av[tb], acc[p], 0, 0, 0);
+            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(val[ta], val[tb], acc[p], 0, 0, 0);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();    // the tile is consumed before the next round rewrites it
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    double* out = slot < 0 ? gram + (int64_t)e * GSP : part + (int64_t)slot * GSP;
+    double* out = slot < 0 ? GSd.gram[sd] + (int64_t)e * GSP : GSd.part[sd] + (int64_t)slot * GSP;
     int p = 0;
 #pragma unroll
     for (int ta = 0; ta < NT; ++ta)
@@ -1017,8 +1038,8 @@ __global__ __launch_bounds__(256) void k_gram_ncf_mfma(
       for (int tb = ta; tb < NT; ++tb, ++p)
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int ci = 16 * ta + grp + 4 * rr;    // C row -> Gram column index (tile ta)
-          const int rj = 16 * tb + col;             // C col -> Gram row index (tile tb)
+          const int ci = 16 * ta + kq + 4 * rr;    // C row -> Gram column index (tile ta)
+          const int rj = 16 * tb + m;              // C col -> Gram row index (tile tb)
           if (rj >= ci) out[tri(rj, ci)] = acc[p][rr];
         }
   }
@@ -1837,46 +1858,44 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   // of split lists (GSP doubles each) stay a few bytes per rating (MI355X: ml-1m-ex MF k=16
   // best at 256, 20M MF k=64 loses 30% at 256 vs 512)
   {
-    int64_t want = M::ncf ? 512 : 256;
-    while (!M::ncf && want < 4096 && want < GSP) want *= 2;
+    int64_t want = 256;
+    while (want < 4096 && want < GSP) want *= 2;
     want = gram_chunk(want);
     if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want));
   }
   const Index& X = c->idx;
   for (int sd = 0; sd < 2; ++sd)
     if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
+  GramSides G;
+  for (int sd = 0; sd < 2; ++sd) {
+    G.n_items[sd] = n_ent[sd] > 0 ? X.n_gitems[sd] : 0;
+    G.items[sd] = X.gitems[sd].as<int32_t>();
+    G.ptr[sd] = X.side[sd].ptr.as<int64_t>();
+    G.other[sd] = X.side[sd].other.as<int32_t>();
+    G.emb_other[sd] = M::ncf ? c->p.t[sd == 0 ? 3 : 2] : c->p.t[sd == 0 ? 1 : 0];   // NCF: gmf tables
+    G.gram[sd] = c->gram[sd].as<double>();
+    G.part[sd] = c->gpart[sd].as<double>();
+    G.lgm[sd] = c->gm[sd].as<double>();
+  }
+  G.W3 = c->p.t[8];
+  G.N = X.N;
   if constexpr (M::ncf) {
+    // per list position of each side: g_mlp (coordinate-major) and e, with the Grams
     const int64_t N = X.N;
     for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1)));
     FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * N + 1)));
-    FIA_HIP_TRY(c->wf64.reserve(sizeof(double) * NCFW64<K>::SIZE));
-    hipLaunchKernelGGL(k_ncf_weights_f64<K>, dim3(1), dim3(256), 0, s, c->p.t[4], c->p.t[5], c->p.t[6], c->p.t[7],
-                       c->p.t[8], c->wf64.as<double>());
-    FIA_HIP_TRY(hipGetLastError());
-    for (int sd = 0; sd < 2; ++sd) {
-      if (n_ent[sd] == 0 || X.n_gitems[sd] == 0) continue;
-      constexpr int WAVES = NCFGramCfg<M>::WAVES;
-      int64_t grid = (X.n_gitems[sd] + WAVES - 1) / WAVES;
-      if (grid > 16384) grid = 16384;
-      hipLaunchKernelGGL(k_gram_ncf_mfma<M>, dim3((unsigned)grid), dim3(64 * WAVES), 0, s, sd, X.n_gitems[sd],
-                         X.gitems[sd].as<int32_t>(), X.side[sd].ptr.as<int64_t>(), X.side[sd].other.as<int32_t>(),
-                         c->p.t[sd == 0 ? 3 : 2], c->l1[sd].as<double>(), c->l1[1 - sd].as<double>(),
-                         c->wf64.as<double>(), c->gram[sd].as<double>(), c->gpart[sd].as<double>(),
-                         c->p.t[sd == 0 ? 2 : 3], X.side[sd].rating.as<float>(), c->p.t[9], N,
-                         c->gm[sd].as<double>(), c->resid.as<double>() + sd * N);
+    for (int sd = 0; sd < 2; ++sd) G.lgm[sd] = c->gm[sd].as<double>();
+    const int64_t n_all = G.n_items[0] + G.n_items[1];
+    if (n_all > 0) {
+      // persistent: the per-lane weight operands are loaded once per wave
+      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;
+      const int64_t grid = n_all < cap ? n_all : cap;
+      hipLaunchKernelGGL(k_ncf_gram_rows<M>, dim3((unsigned)grid), dim3(64), 0, s, G, c->p.t[4], c->p.t[5],
+                         c->p.t[6], c->p.t[7], c->p.t[9], c->l1[0].as<double>(), c->l1[1].as<double>(),
+                         X.side[0].rating.as<float>(), X.side[1].rating.as<float>(), c->resid.as<double>());
       FIA_HIP_TRY(hipGetLastError());
     }
   } else {
-    GramSides G;
-    for (int sd = 0; sd < 2; ++sd) {
-      G.n_items[sd] = n_ent[sd] > 0 ? X.n_gitems[sd] : 0;
-      G.items[sd] = X.gitems[sd].as<int32_t>();
-      G.ptr[sd] = X.side[sd].ptr.as<int64_t>();
-      G.other[sd] = X.side[sd].other.as<int32_t>();
-      G.emb_other[sd] = c->p.t[sd == 0 ? 1 : 0];
-      G.gram[sd] = c->gram[sd].as<double>();
-      G.part[sd] = c->gpart[sd].as<double>();
-    }
     if (G.n_items[0] + G.n_items[1] > 0) {
       hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
       FIA_HIP_TRY(hipGetLastError());
