@@ -956,13 +956,44 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
     d4_t acc[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
+    // Software pipeline over the slabs: the list ids run two slabs ahead and the gathers
+    // one slab ahead (they only depend on the ids), so a slab waits on no memory round trip.
+    // Per slab and lane: lo = L1_other[o_m][kq + 4kk], gf = Go[o_m][kq + 4kk] (residual),
+    // gg[r][t] = Go[o_(4r+kq)][16t + m - k] (Gram operand of the gmf coordinates).
+    const int lastp = len - 1;
+    int32_t o = ids[m < lastp ? m : lastp];
+    int32_t o_n = ids[16 + m < lastp ? 16 + m : lastp];
+    double lo[KK];
+    float gf[KK], gg[4][NT];
+    auto gather = [&](int32_t oo, double (&lo_)[KK], float (&gf_)[KK], float (&gg_)[4][NT]) {
+      const double* __restrict__ Lo = L1o + (int64_t)oo * K;
+      const float* __restrict__ Gom = Go + (int64_t)oo * K;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        lo_[kk] = Lo[kq + 4 * kk];
+        gf_[kk] = Gom[kq + 4 * kk];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int32_t orow = __shfl(oo, 4 * r + kq);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int co = 16 * t + m;
+          gg_[r][t] = 0.f;
+          if (16 * t + 15 >= K && co >= K) gg_[r][t] = Go[(int64_t)orow * K + co - K];
+        }
+      }
+    };
+    gather(o, lo, gf, gg);
     for (int s0 = 0; s0 < len; s0 += 16) {
       const bool ok = s0 + m < len;
-      const int32_t o = ids[ok ? s0 + m : 0];
-      const double* __restrict__ Lo = L1o + (int64_t)o * K;
+      const int32_t o_nn = ids[s0 + 32 + m < lastp ? s0 + 32 + m : lastp];
+      double lo_n[KK];
+      float gf_n[KK], gg_n[4][NT];
+      gather(o_n, lo_n, gf_n, gg_n);       // next slab (a harmless repeat past the end)
       double z1[KK];
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) z1[kk] = ok ? zs[kk] + Lo[kq + 4 * kk] : 0.0;
+      for (int kk = 0; kk < KK; ++kk) z1[kk] = ok ? zs[kk] + lo[kk] : 0.0;
       d4_t z2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk)
@@ -994,10 +1025,9 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
         for (int kk = 0; kk < KK; ++kk) gm[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(d1[kk], aW1[t][kk], gm[t], 0, 0, 0);
       }
       // residual of position m (mlp and the gmf dot are split over the 4 lane groups)
-      const float* __restrict__ Gom = Go + (int64_t)o * K;
       double gmf = 0.0;
 #pragma unroll
-      for (int kk = 0; kk < KK; ++kk) gmf = fma(gsk[kk], (double)Gom[kq + 4 * kk], gmf);
+      for (int kk = 0; kk < KK; ++kk) gmf = fma(gsk[kk], (double)gf[kk], gmf);
       double re = mlp + gmf;
       re += __shfl_xor(re, 16);
       re += __shfl_xor(re, 32);
@@ -1007,18 +1037,17 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
       for (int r = 0; r < 4; ++r) {
         const int pr = s0 + 4 * r + kq;
         const bool okr = pr < len;
-        const int32_t orow = __shfl(o, 4 * r + kq);
         double val[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const int co = 16 * t + m;
           const double gv = gm[t < KT ? t : KT - 1][r];
-          double x = 0.0;
+          double x;
           if (co < K) {
             x = gv;
             if (okr) lgp[(int64_t)co * N + pr] = gv;
-          } else if (okr) {
-            x = w3gt[t] * (double)Go[(int64_t)orow * K + co - K];
+          } else {
+            x = w3gt[t] * (double)gg[r][t];
           }
           val[t] = okr ? x : 0.0;
         }
@@ -1029,6 +1058,16 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
           for (int tb = ta; tb < NT; ++tb, ++p)
             acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(val[ta], val[tb], acc[p], 0, 0, 0);
       }
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        lo[kk] = lo_n[kk];
+        gf[kk] = gf_n[kk];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) gg[r][t] = gg_n[r][t];
+      o_n = o_nn;
     }
     double* out = slot < 0 ? GSd.gram[sd] + (int64_t)e * GSP : GSd.part[sd] + (int64_t)slot * GSP;
     int p = 0;
@@ -1859,7 +1898,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   // best at 256, 20M MF k=64 loses 30% at 256 vs 512)
   {
     int64_t want = 256;
-    while (want < 4096 && want < GSP) want *= 2;
+    while (!M::ncf && want < 4096 && want < GSP) want *= 2;   // NCF: 256 (16 slabs per item)
     want = gram_chunk(want);
     if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want));
   }
@@ -1888,7 +1927,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
     const int64_t n_all = G.n_items[0] + G.n_items[1];
     if (n_all > 0) {
       // persistent: the per-lane weight operands are loaded once per wave
-      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;
+      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 8;
       const int64_t grid = n_all < cap ? n_all : cap;
       hipLaunchKernelGGL(k_ncf_gram_rows<M>, dim3((unsigned)grid), dim3(64), 0, s, G, c->p.t[4], c->p.t[5],
                          c->p.t[6], c->p.t[7], c->p.t[9], c->l1[0].as<double>(), c->l1[1].as<double>(),
