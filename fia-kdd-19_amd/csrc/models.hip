@@ -286,9 +286,10 @@ __device__ void ldlt_cols(double* __restrict__ Hb, double* __restrict__ vb) {
 // by the rank-1 update.  (A v_readlane / ds_bpermute per element costs N^2/2 serialised
 // broadcasts: NCF k=16 spent 0.84 ms of 0.95 there.)  After step j lane c > j keeps
 // L[c][j] in col[j] (forward solve) and its own column below the diagonal holds
-// d_c L[r][c] (backward solve); the two triangular solves broadcast one value per step
+// d_c L[r][c] (backward solve).  The forward solve L y = g rides along (lane j publishes
+// y_j with the pivot column); the backward solve broadcasts one value per step
 // by v_readlane.  g: right-hand sides [2N] (LDS), v: solutions [2N] (LDS),
-// P: pivot-column staging [64] (LDS).
+// P: pivot-column staging [68] (LDS).
 template <int N>
 __device__ __forceinline__ double bcast_col(double x, int j) {
   if constexpr (2 * N <= 64) {
@@ -329,7 +330,10 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
     const int c = PAR ? lane & 31 : lane;
     const bool live = c < N;
     const double* __restrict__ Gb = Hs + b * GS;
-    double* __restrict__ Pb = P + b * 32;     // 64 slots: every lane publishes unconditionally
+    // column slots (one per lane of the block) + y_j + a dummy slot; every lane publishes.
+    // PAR: the halves use [0, 34) and [34, 68); otherwise the blocks run in turn on [0, 66)
+    constexpr int YS = PAR ? 32 : 64;
+    double* __restrict__ Pb = P + (PAR ? b * 34 : 0);
     double col[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) {
@@ -344,10 +348,16 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       Pb[c] = col[j];                           // A[c][j] (= col[j] by symmetry); rows >= j read
+      Pb[c == j ? YS : YS + 1] = y;             // y_j is final: the forward solve rides along
+                                                // (slot 33: the other lanes' unconditional store)
       wave_lds_sync();
-      const double ij = 1.0 / Pb[j];
+      const double dj = Pb[j];
+      double ij = __builtin_amdgcn_rcp(dj);     // 1/d_j: v_rcp_f64 + two Newton steps
+      ij = fma(ij, fma(-dj, ij, 1.0), ij);
+      ij = fma(ij, fma(-dj, ij, 1.0), ij);
       if (c == j) dinv_own = ij;
       const double f = c > j ? col[j] * ij : 0.0;
+      y = fma(-f, Pb[YS], y);                   // L y = g, column j
       // fixed trip count: the inner loop unrolls before the outer one, so a j-dependent
       // bound would leave col[] indexed at run time (scratch)
 #pragma unroll
@@ -356,20 +366,11 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
       if (c > j) col[j] = f;
       wave_lds_sync();                          // this step's reads before the next writes
     }
-#pragma unroll
-    for (int i = 0; i < N; ++i) {             // L y = g
-      int ci = c;
-      asm volatile("" : "+v"(ci));
-      const double yi = bcast_col<N>(y, i);
-      if (ci > i) y = fma(-col[i], yi, y);
-    }
     y *= dinv_own;
 #pragma unroll
     for (int j = N - 1; j >= 0; --j) {        // L^T x = D^-1 y
-      int cj = c;
-      asm volatile("" : "+v"(cj));
       const double xj = bcast_col<N>(y, j);
-      if (cj < j) y = fma(-col[j] * dinv_own, xj, y);
+      if (c < j) y = fma(-col[j] * dinv_own, xj, y);
     }
     if (live) v[b * N + c] = y;
   }
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t
                                                          int32_t* __restrict__ coupled_out) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
   __shared__ double H[COLS ? 2 * GS : D * (D + 1) / 2];
-  __shared__ double v[D], g[D], th[D], dd[D], ww[D], pv[64];
+  __shared__ double v[D], g[D], th[D], dd[D], ww[D], pv[68];
   __shared__ double sh[4 * K + 8];
   // NCF weights staged once per block (fp64), read by every query the block solves
   __shared__ NCFWeights<M::ncf ? K : 2> w;
