@@ -113,7 +113,7 @@ int fia_destroy(fia_ctx* c) {
       c->bitems[s].release();
       c->bcomb[s].release();
     }
-    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->scan_tmp,
+    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->scan_tmp, &c->qscan,
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
                            &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->wcnt,
                            &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,

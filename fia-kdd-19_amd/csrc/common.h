@@ -154,6 +154,7 @@ struct fia_ctx {
   fia::DevBuf cand_pos;   // int32 [max chunks * K]
   fia::DevBuf cand_val;   // double [max chunks * K]
   fia::DevBuf scan_tmp;   // rocprim temporary storage
+  fia::DevBuf qscan;      // k_query_scan tile words + counters (left zero by every launch)
   fia::DevBuf flag;       // int32 [4] device status words
   fia::DevBuf nch;        // int64 [Q+1] chunk counts
   fia::DevBuf coupled;    // int32 [Q + 1]: count, then queries whose test pair is a train row
@@ -204,7 +205,7 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
                          const int64_t* offsets, int64_t* rel, hipStream_t s);
 // per-query chunk offsets coff (+ chunk descriptors unless offsets_only)
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, bool offsets_only, hipStream_t s);
+                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk);
 int64_t gram_chunk(int64_t want);
 hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);

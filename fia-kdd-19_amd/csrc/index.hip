@@ -76,20 +76,6 @@ __global__ void k_list_ptr(const int32_t* __restrict__ keys, int64_t N, int64_t 
   ptr[e] = lo;
 }
 
-__global__ void k_count(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
-                        const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
-                        int64_t* __restrict__ counts, int32_t* __restrict__ flag) {
-  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q > Q) return;
-  if (q == Q) { counts[Q] = 0; return; }
-  int32_t u = qu[q], i = qi[q];
-  int64_t n = 0;
-  bool ok = (u >= 0 && u < U && i >= 0 && i < I);
-  if (ok) n = (uptr[u + 1] - uptr[u]) + (iptr[i + 1] - iptr[i]);
-  else atomicOr(flag + 1, 1);
-  counts[q] = n;
-}
-
 __device__ inline void query_sides(const int32_t* qu, const int32_t* qi, int64_t q, const int64_t* uptr,
                                    const int64_t* iptr, int64_t U, int64_t I, int64_t& ub, int64_t& du, int64_t& ib,
                                    int64_t& di) {
@@ -103,47 +89,144 @@ __device__ inline void query_sides(const int32_t* qu, const int32_t* qi, int64_t
   }
 }
 
-// chunks per query: ceil(|R_u| / kChunk) + ceil(|C_i| / kChunk)
-__global__ void k_chunk_counts(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
-                               const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U,
-                               int64_t I, int64_t* __restrict__ nch) {
-  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q > Q) return;
-  if (q == Q) { nch[Q] = 0; return; }
-  int64_t ub, du, ib, di;
-  query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
-  nch[q] = (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
-}
+// ---- single-pass per-query scans (decoupled look-back) ----
+// One launch replaces count kernel + two-kernel library scan (+ descriptor fill): tiles of
+// kScanTile queries take a dynamic tile number, publish their aggregate, look back over
+// the earlier tiles' words {flag (2 bits), value (62 bits)} and write the exclusive
+// prefix of every query (+ the total at [Q]).  The last tile to finish clears the tile
+// words and counters, so no memset precedes the next launch.
+//   MODE 0: n_q = |R_u| + |C_i| -> offsets (fia_count_related); bad ids flag[1]
+//   MODE 1: chunks_q = ceil(|R_u|/kChunk) + ceil(|C_i|/kChunk) -> coff, + chunk descriptors
+constexpr int kScanThreads = 256, kScanItems = 1, kScanTile = kScanThreads * kScanItems;
+constexpr unsigned long long kScanAgg = 1ull << 62, kScanPre = 2ull << 62, kScanVal = (1ull << 62) - 1;
 
-__global__ void k_chunk_fill(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
-                             const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
-                             const int64_t* __restrict__ offsets, const int64_t* __restrict__ coff,
-                             ChunkDesc* __restrict__ cdesc) {
-  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= Q) return;
-  int64_t ub, du, ib, di;
-  query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
-  int64_t c = coff[q];
-  const int64_t base = offsets[q];
-  for (int64_t st = 0; st < du; st += kChunk, ++c) {
-    ChunkDesc d;
-    d.list_base = ub + st;
-    d.out_base = base + st;
-    d.q = (int32_t)q;
-    d.pos0 = (int32_t)st;
-    d.len = (int32_t)(du - st < kChunk ? du - st : kChunk);
-    d.side = 0;
-    cdesc[c] = d;
+template <int MODE>
+__global__ __launch_bounds__(kScanThreads) void k_query_scan(
+    const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q, const int64_t* __restrict__ uptr,
+    const int64_t* __restrict__ iptr, int64_t U, int64_t I, int64_t* __restrict__ out,
+    unsigned long long* __restrict__ tstate, unsigned int* __restrict__ tctr, int32_t* __restrict__ flag,
+    const int64_t* __restrict__ offsets, ChunkDesc* __restrict__ cdesc, int32_t* __restrict__ zero_word) {
+  __shared__ int s_tile;
+  __shared__ int64_t s_wave[kScanThreads / 64];
+  __shared__ int64_t s_prefix;
+  const unsigned ntiles = (unsigned)((Q + 1 + kScanTile - 1) / kScanTile);
+  if (threadIdx.x == 0) s_tile = (int)atomicAdd(&tctr[0], 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t q0 = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int64_t v[kScanItems];
+  int64_t tsum = 0;
+#pragma unroll
+  for (int it = 0; it < kScanItems; ++it) {
+    const int64_t q = q0 + it;
+    int64_t x = 0;
+    if (q < Q) {
+      const int32_t u = qu[q], i = qi[q];
+      if (u >= 0 && u < U && i >= 0 && i < I) {
+        const int64_t du = uptr[u + 1] - uptr[u], di = iptr[i + 1] - iptr[i];
+        x = MODE == 0 ? du + di : (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
+      } else if (MODE == 0) {
+        atomicOr(flag + 1, 1);
+      }
+    }
+    v[it] = x;
+    tsum += x;
   }
-  for (int64_t st = 0; st < di; st += kChunk, ++c) {
-    ChunkDesc d;
-    d.list_base = ib + st;
-    d.out_base = base + du + st;
-    d.q = (int32_t)q;
-    d.pos0 = (int32_t)(du + st);
-    d.len = (int32_t)(di - st < kChunk ? di - st : kChunk);
-    d.side = 1;
-    cdesc[c] = d;
+  // block scan of the per-thread sums
+  int64_t inc = tsum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(inc, off);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  int64_t wbase = 0, agg = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / 64; ++w) {
+    if (w < wave) wbase += s_wave[w];
+    agg += s_wave[w];
+  }
+  // publish this tile's aggregate, then look back with the whole first wave: lane l reads
+  // the word of tile (window end - l); the nearest inclusive prefix ends the walk
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&tstate[tile], (tile == 0 ? kScanPre : kScanAgg) | (unsigned long long)agg,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wave == 0) {
+    int64_t excl = 0;
+    for (int64_t end = tile - 1; end >= 0;) {
+      const int64_t p = end - lane;
+      const unsigned long long w =
+          p >= 0 ? __hip_atomic_load(&tstate[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kScanPre;
+      const unsigned long long f = w >> 62;
+      const unsigned long long pre = __ballot(f == 2), inv = __ballot(f == 0);
+      const int stop = pre ? __builtin_ctzll(pre) : 64;            // first lane holding a prefix
+      const unsigned long long need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+      if (inv & need) {                                              // a needed tile not published yet
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      int64_t part = lane <= stop ? (int64_t)(w & kScanVal) : 0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+      excl += part;
+      if (stop < 64) break;
+      end -= 64;
+    }
+    if (lane == 0) {
+      if (tile > 0)
+        __hip_atomic_store(&tstate[tile], kScanPre | (unsigned long long)(excl + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      s_prefix = excl;
+      if (MODE == 1 && tile == 0 && zero_word) zero_word[0] = 0;   // solve's coupled-query counter
+    }
+  }
+  __syncthreads();
+  int64_t run = s_prefix + wbase + inc - tsum;
+#pragma unroll
+  for (int it = 0; it < kScanItems; ++it) {
+    const int64_t q = q0 + it;
+    if (q <= Q) out[q] = run;
+    if (MODE == 1 && cdesc && q < Q && v[it] > 0) {
+      int64_t ub, du, ib, di;
+      query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
+      int64_t c = run;
+      const int64_t base = offsets[q];
+      for (int64_t st = 0; st < du; st += kChunk, ++c) {
+        ChunkDesc d;
+        d.list_base = ub + st;
+        d.out_base = base + st;
+        d.q = (int32_t)q;
+        d.pos0 = (int32_t)st;
+        d.len = (int32_t)(du - st < kChunk ? du - st : kChunk);
+        d.side = 0;
+        cdesc[c] = d;
+      }
+      for (int64_t st = 0; st < di; st += kChunk, ++c) {
+        ChunkDesc d;
+        d.list_base = ib + st;
+        d.out_base = base + du + st;
+        d.q = (int32_t)q;
+        d.pos0 = (int32_t)(du + st);
+        d.len = (int32_t)(di - st < kChunk ? di - st : kChunk);
+        d.side = 1;
+        cdesc[c] = d;
+      }
+    }
+    run += v[it];
+  }
+  // the last tile to finish resets the tile words and the counters for the next launch
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned done = atomicAdd(&tctr[1], 1u);
+    if (done == ntiles - 1) {
+      for (unsigned t = 0; t < ntiles; ++t)
+        __hip_atomic_store(&tstate[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&tctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&tctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -386,16 +469,35 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
   return hipSuccess;
 }
 
+// tile words + two counters of k_query_scan, zero when (re)allocated; every launch leaves
+// them zero again
+static hipError_t scan_state(fia_ctx* c, int64_t Q, hipStream_t s) {
+  const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
+  const size_t need = sizeof(unsigned long long) * (size_t)ntiles + 16;
+  if (c->qscan.bytes >= need && c->qscan.ptr) return hipSuccess;
+  FIA_HIP_TRY(hipStreamSynchronize(s));
+  c->qscan.release();
+  FIA_HIP_TRY(c->qscan.reserve(need < 4096 ? 4096 : need));
+  FIA_HIP_TRY(hipMemsetAsync(c->qscan.ptr, 0, c->qscan.bytes, s));
+  return hipSuccess;
+}
+
+template <int MODE>
+static hipError_t launch_query_scan(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* out,
+                                    const int64_t* offsets, ChunkDesc* cdesc, int32_t* zero_word, hipStream_t s) {
+  FIA_HIP_TRY(scan_state(c, Q, s));
+  FIA_HIP_TRY(c->flag.reserve(64));
+  const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
+  unsigned int* ctr = reinterpret_cast<unsigned int*>(c->qscan.as<char>() + c->qscan.bytes - 16);
+  hipLaunchKernelGGL(k_query_scan<MODE>, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, qu, qi, Q,
+                     c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I, out,
+                     c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word);
+  return hipGetLastError();
+}
+
 hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* offsets,
                          hipStream_t s) {
-  // counts go to the chunk-offset scratch, then an exclusive scan into offsets
-  FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
-  FIA_HIP_TRY(c->flag.reserve(64));
-  hipLaunchKernelGGL(k_count, dim3((unsigned)((Q + 1 + 255) / 256)), dim3(256), 0, s, qu, qi, Q,
-                     c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I,
-                     c->coff.as<int64_t>(), c->flag.as<int32_t>());
-  FIA_HIP_TRY(hipGetLastError());
-  return exclusive_scan_i64(c, c->coff.as<int64_t>(), offsets, Q + 1, s);
+  return launch_query_scan<0>(c, Q, qu, qi, offsets, nullptr, nullptr, nullptr, s);
 }
 
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
@@ -408,23 +510,11 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 }
 
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, bool offsets_only, hipStream_t s) {
+                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
   if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1)));
-  FIA_HIP_TRY(c->nch.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
-  int64_t* nch = c->nch.as<int64_t>();
-  const int64_t* uptr = c->idx.side[0].ptr.as<int64_t>();
-  const int64_t* iptr = c->idx.side[1].ptr.as<int64_t>();
-  hipLaunchKernelGGL(k_chunk_counts, dim3((unsigned)((Q + 1 + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr,
-                     c->idx.U, c->idx.I, nch);
-  FIA_HIP_TRY(hipGetLastError());
-  FIA_HIP_TRY(exclusive_scan_i64(c, nch, c->coff.as<int64_t>(), Q + 1, s));
-  if (Q > 0 && !offsets_only) {
-    hipLaunchKernelGGL(k_chunk_fill, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr,
-                       c->idx.U, c->idx.I, offsets, c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>());
-    FIA_HIP_TRY(hipGetLastError());
-  }
-  return hipSuccess;
+  return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
+                              offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s);
 }
 
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,

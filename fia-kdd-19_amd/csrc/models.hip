@@ -1972,15 +1972,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int64_t nE = c->idx.U + c->idx.I;
   // every (entity chunk, query block) item covers >= 1 per-query chunk
   const int64_t max_items = max_chunks;
+  // the queries whose test pair is a train row are listed in `coupled` {count, q...} by the
+  // solve and finished full-D; the chunk scan zeroes the count
+  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
   phase_begin(c, 4, s);
-  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s));
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, kQueryBlock, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
-  // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks; the
-  // queries whose test pair is a train row are listed in `coupled` and solved full-D
-  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
-  FIA_HIP_TRY(hipMemsetAsync(c->coupled.ptr, 0, sizeof(int32_t), s));
+  // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
   if (Q > 0) {
     static const bool tps_on = !getenv("FIA_NO_TPS");   // A/B knob: wave-per-query solve instead
     if (use_tps<M>() && tps_on) {
