@@ -219,7 +219,8 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   // the last tile to finish resets the tile words and the counters for the next launch
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
+    // (no fence: the tile words this block read were consumed before this point, and the
+    // outputs are read by later kernels only)
     const unsigned done = atomicAdd(&tctr[1], 1u);
     if (done == ntiles - 1) {
       for (unsigned t = 0; t < ntiles; ++t)

@@ -780,11 +780,12 @@ struct GramSides {
   const float* emb_other[2];
   double* gram[2];
   double* part[2];
-  // NCF (k_gram_ncf_rows): stored g_mlp rows per side, W3, list length N
+  // NCF (k_ncf_gram_rows): stored g_mlp rows per side, W3, list length N
   const double* lgm[2];
   const float* W3;
   int64_t N;
 };
+
 
 template <class M>
 __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
@@ -811,11 +812,12 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
   double sum[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) sum[t] = 0.0;
-  for (int t0 = 0; t0 < len; t0 += 4 * SUB) {
-    // one coalesced load of 4*SUB row ids, then every row-quad's gather in flight at once
-    const int my = t0 + lane;
-    const int32_t id = (lane < 4 * SUB && my < len) ? ids[my] : -1;
-    double val[SUB][NT];
+  // one coalesced load of 4*SUB row ids per batch, every row-quad's gather in flight at
+  // once.  k >= 32: software-pipelined (ids two batches ahead, gathers one batch ahead;
+  // 20M MF k=64 prepare 8.0 -> 6.7 ms); k <= 16 lists are mostly one or two batches and
+  // the look-ahead costs more than it hides (ml-1m-ex 57 -> 65 us)
+  auto ids_at = [&](int t0) -> int32_t { return (lane < 4 * SUB && t0 + lane < len) ? ids[t0 + lane] : -1; };
+  auto gather = [&](int32_t id, double (&val)[SUB][NT]) {
 #pragma unroll
     for (int sb = 0; sb < SUB; ++sb) {
       const int32_t o = __shfl(id, 4 * sb + grp);
@@ -823,6 +825,8 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) val[sb][t] = (o >= 0 && 16 * t + col < K) ? (double)src[16 * t + col] : 0.0;
     }
+  };
+  auto accumulate = [&](const double (&val)[SUB][NT]) {
 #pragma unroll
     for (int sb = 0; sb < SUB; ++sb) {
       int p = 0;
@@ -833,6 +837,28 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
         for (int tb = ta; tb < NT; ++tb, ++p)
           acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(val[sb][ta], val[sb][tb], acc[p], 0, 0, 0);
       }
+    }
+  };
+  if constexpr (K >= 32) {
+    double val[SUB][NT];
+    gather(ids_at(0), val);
+    int32_t id_n = ids_at(4 * SUB);
+    for (int t0 = 0; t0 < len; t0 += 4 * SUB) {
+      const int32_t id_nn = ids_at(t0 + 8 * SUB);
+      double vn[SUB][NT];
+      gather(id_n, vn);                          // next batch (ids -1 past the end)
+      accumulate(val);
+#pragma unroll
+      for (int sb = 0; sb < SUB; ++sb)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) val[sb][t] = vn[sb][t];
+      id_n = id_nn;
+    }
+  } else {
+    for (int t0 = 0; t0 < len; t0 += 4 * SUB) {
+      double val[SUB][NT];
+      gather(ids_at(t0), val);
+      accumulate(val);
     }
   }
   double* out = slot < 0 ? gram + (int64_t)e * GSP : part + (int64_t)slot * GSP;
