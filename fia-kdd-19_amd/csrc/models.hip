@@ -664,6 +664,17 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
     else
       u = i = 0;
   }
+  const int32_t ent = side == 0 ? u : i;       // this block's entity
+  const int32_t oth = side == 0 ? i : u;       // the other endpoint of the test pair
+  const float* Eself = side == 0 ? A.t[0] : A.t[1];
+  const float* Eoth = side == 0 ? A.t[1] : A.t[0];
+  const float* Bself = side == 0 ? A.t[2] : A.t[3];
+  // the cached block's loads go out first: they overlap the pair lookup's probe chain
+  const double* G = A.gram[side] + (int64_t)ent * GSP;
+  double h[GS];
+#define HS(t) h[(t)]
+#pragma unroll
+  for (int t = 0; t < GS; ++t) HS(t) = G[t];
   double cdup = 0.0, rsum = 0.0;
   if (active && n > 0)
     A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
@@ -677,20 +688,12 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
     if (side == 0) rec[q * M::R] = NAN;
   }
   const bool work = active && n > 0 && cdup == 0.0;
-  const int32_t ent = side == 0 ? u : i;       // this block's entity
-  const int32_t oth = side == 0 ? i : u;       // the other endpoint of the test pair
-  const float* Eself = side == 0 ? A.t[0] : A.t[1];
-  const float* Eoth = side == 0 ? A.t[1] : A.t[0];
-  const float* Bself = side == 0 ? A.t[2] : A.t[3];
 
-  // H block = (2/n) Gram + wd on the embedding coordinates + damping
+  // H block = (2/n) Gram + wd on the embedding coordinates + damping, in registers (fully
+  // unrolled, every index constant)
   const double s2n = n > 0 ? 2.0 / (double)n : 0.0;
-  const double* G = A.gram[side] + (int64_t)ent * GSP;
-  // the whole packed block lives in registers: fully unrolled, every index constant
-  double h[GS];
-#define HS(t) h[(t)]
 #pragma unroll
-  for (int t = 0; t < GS; ++t) HS(t) = s2n * G[t];
+  for (int t = 0; t < GS; ++t) HS(t) *= s2n;
 #pragma unroll
   for (int r = 0; r < Ds; ++r) HS(tri(r, r)) += (r < K ? A.wd : 0.0) + A.damping;
 
