@@ -1566,96 +1566,115 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    double ea[RT], acc[QB][RT];
+    // NQ = nq rounded up to a power of two: a static query count per path keeps the
+    // accumulators in registers without per-query exits (padding columns score copies of
+    // the last query and are never written out).  The embedding chunk of the next step is
+    // gathered while this step's FMAs run.
+    auto run = [&](auto nq_c) {
+      constexpr int NQ = decltype(nq_c)::value;
+      double ea[RT], acc[NQ][RT];
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      ea[r] = 0.0;
+      for (int r = 0; r < RT; ++r) {
+        ea[r] = 0.0;
 #pragma unroll
-      for (int j = 0; j < QB; ++j) acc[j][r] = 0.0;
-    }
-#pragma unroll 1
-    for (int c0 = 0; c0 < K; c0 += CK) {
+        for (int j = 0; j < NQ; ++j) acc[j][r] = 0.0;
+      }
+      auto gather = [&](int c0, float (&g)[RT][CK]) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + c0);
+          const float4 a = src[0], b = src[1];
+          g[r][0] = a.x; g[r][1] = a.y; g[r][2] = a.z; g[r][3] = a.w;
+          g[r][4] = b.x; g[r][5] = b.y; g[r][6] = b.z; g[r][7] = b.w;
+        }
+      };
       float ga[RT][CK];
+      gather(0, ga);
+#pragma unroll 1
+      for (int c0 = 0; c0 < K; c0 += CK) {
+        float gn[RT][CK];
+        gather(c0 + CK < K ? c0 + CK : c0, gn);
 #pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + c0);
-        const float4 a = src[0], b = src[1];
-        ga[r][0] = a.x; ga[r][1] = a.y; ga[r][2] = a.z; ga[r][3] = a.w;
-        ga[r][4] = b.x; ga[r][5] = b.y; ga[r][6] = b.z; ga[r][7] = b.w;
-      }
+        for (int cc = 0; cc < CK; ++cc) {
+          const double sc = SV(c0 + cc);
 #pragma unroll
-      for (int cc = 0; cc < CK; ++cc) {
-        const double sc = SV(c0 + cc);
-#pragma unroll
-        for (int r = 0; r < RT; ++r) ea[r] = fma(sc, (double)ga[r][cc], ea[r]);
-      }
-#pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        if (j >= nq) break;
-        const double2* __restrict__ xr = reinterpret_cast<const double2*>(rl + j * RSW + 4 + K + c0);
-#pragma unroll
-        for (int c2 = 0; c2 < CK / 2; ++c2) {
-          const double2 x2 = xr[c2];
-#pragma unroll
-          for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.x, (double)ga[r][2 * c2], acc[j][r]);
-#pragma unroll
-          for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.y, (double)ga[r][2 * c2 + 1], acc[j][r]);
+          for (int r = 0; r < RT; ++r) ea[r] = fma(sc, (double)ga[r][cc], ea[r]);
         }
-      }
-    }
-    {
-      const double gbias = (double)A.t[4][0];
-      const double bself = SV(K);
 #pragma unroll
-      for (int r = 0; r < RT; ++r) ea[r] = ea[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
-    }
-#undef SV
+        for (int j = 0; j < NQ; ++j) {
+          const double2* __restrict__ xr = reinterpret_cast<const double2*>(rl + j * RSW + 4 + K + c0);
 #pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      if (j >= nq) break;
-      const double* __restrict__ Rj = rl + j * RSW;
-      const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
-      const double xsb = Rj[4 + 2 * K + 1], dup_o = Rj[4 + 2 * K + 2];
-      const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
-      double la[RT], lv[RT];
-      int lp[RT];
+          for (int c2 = 0; c2 < CK / 2; ++c2) {
+            const double2 x2 = xr[c2];
 #pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        double ee = ea[r], ss = acc[j][r] + xsb;
-        if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
-        const double infl = (2.0 * ee * ss + cq) * inv_n;
-        const int idx = r * 64 + lane;
-        if (ok_[r]) {
-          if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-          if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
-        }
-        lp[r] = ok_[r] ? cidx * kChunk + idx : -1;
-        la[r] = ok_[r] ? topk_key(infl) : -2.0;
-        lv[r] = infl;
-      }
-      if (K_top > 0) {
-        double pa = INFINITY;
-        int pp = -1;
-        for (int t = 0; t < K_top; ++t) {
-          double ba = -2.0, bv = 0.0;
-          int bp = 0x7fffffff;
+            for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.x, (double)ga[r][2 * c2], acc[j][r]);
 #pragma unroll
-          for (int r = 0; r < RT; ++r)
-            if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
-              ba = la[r]; bp = lp[r]; bv = lv[r];
-            }
-          wave_best(ba, bp, bv);
-          if (lane == 0) {
-            const bool okk = ba > -1.5;
-            const int64_t slot = cbj * K_top + t;
-            cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
-            cand_val[slot] = okk ? bv : NAN;
+            for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.y, (double)ga[r][2 * c2 + 1], acc[j][r]);
           }
-          pa = ba;
-          pp = bp;
+        }
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+#pragma unroll
+          for (int cc = 0; cc < CK; ++cc) ga[r][cc] = gn[r][cc];
+      }
+      {
+        const double gbias = (double)A.t[4][0];
+        const double bself = SV(K);
+#pragma unroll
+        for (int r = 0; r < RT; ++r) ea[r] = ea[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
+      }
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        if (j >= nq) continue;
+        const double* __restrict__ Rj = rl + j * RSW;
+        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
+        const double xsb = Rj[4 + 2 * K + 1], dup_o = Rj[4 + 2 * K + 2];
+        const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
+        double la[RT], lv[RT];
+        int lp[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          double ee = ea[r], ss = acc[j][r] + xsb;
+          if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
+          const double infl = (2.0 * ee * ss + cq) * inv_n;
+          const int idx = r * 64 + lane;
+          if (ok_[r]) {
+            if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
+            if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+          }
+          lp[r] = ok_[r] ? cidx * kChunk + idx : -1;
+          la[r] = ok_[r] ? topk_key(infl) : -2.0;
+          lv[r] = infl;
+        }
+        if (K_top > 0) {
+          double pa = INFINITY;
+          int pp = -1;
+          for (int t = 0; t < K_top; ++t) {
+            double ba = -2.0, bv = 0.0;
+            int bp = 0x7fffffff;
+#pragma unroll
+            for (int r = 0; r < RT; ++r)
+              if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
+                ba = la[r]; bp = lp[r]; bv = lv[r];
+              }
+            wave_best(ba, bp, bv);
+            if (lane == 0) {
+              const bool okk = ba > -1.5;
+              const int64_t slot = cbj * K_top + t;
+              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+              cand_val[slot] = okk ? bv : NAN;
+            }
+            pa = ba;
+            pp = bp;
+          }
         }
       }
-    }
+    };
+    if (nq <= 1) run(std::integral_constant<int, 1>{});
+    else if (nq <= 2) run(std::integral_constant<int, 2>{});
+    else if (nq <= 4) run(std::integral_constant<int, 4>{});
+    else run(std::integral_constant<int, QB>{});
+#undef SV
     __builtin_amdgcn_wave_barrier();
   }
 }
