@@ -311,7 +311,13 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
                                   double wd, double damping, const double* __restrict__ g, double* __restrict__ v,
                                   double* __restrict__ Hs, double* __restrict__ P) {
   constexpr int N = M::Ds, GS = N * (N + 1) / 2;
-  static_assert(N <= 64, "one column per lane");
+  // N = 65 (MF k=64: 64 embedding coordinates + the bias): the 64 lanes own columns 0..63
+  // and the bias coordinate rides along -- its row is the last entry of every column, its
+  // pivot-row entry is published by the pivot lane, and its own diagonal and right-hand
+  // side are carried redundantly by every lane (a Schur complement, one step per column)
+  constexpr bool EXTRA = N == 65;
+  constexpr int NC = EXTRA ? 64 : N;            // lane-owned columns
+  static_assert(N <= 65, "one column per lane (+ the MF bias)");
   constexpr bool PAR = 2 * N <= 64;
   // lane-derived values are made opaque where they are used, so the compiler does not
   // hoist N column addresses and N lane masks out of the caller's query loop (spills)
@@ -328,11 +334,13 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
   for (int b0 = 0; b0 < (PAR ? 1 : 2); ++b0) {
     const int b = PAR ? lane >> 5 : b0;
     const int c = PAR ? lane & 31 : lane;
-    const bool live = c < N;
+    const bool live = c < NC;
     const double* __restrict__ Gb = Hs + b * GS;
     // column slots (one per lane of the block) + y_j + a dummy slot; every lane publishes.
     // PAR: the halves use [0, 34) and [34, 68); otherwise the blocks run in turn on [0, 66)
-    constexpr int YS = PAR ? 32 : 64;
+    // (EXTRA: [0, 68) with the bias row entry at 64 and y_j at 66)
+    constexpr int XS = 64;
+    constexpr int YS = EXTRA ? 66 : PAR ? 32 : 64;
     double* __restrict__ Pb = P + (PAR ? b * 34 : 0);
     double col[N];
 #pragma unroll
@@ -345,11 +353,15 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
       if (r == c) col[r] += (M::decayed(r) ? wd : 0.0) + damping;
     double y = live ? g[b * N + c] : 0.0;
     double dinv_own = 0.0;
+    // EXTRA: the bias coordinate's pivot and right-hand side (identical in every lane)
+    double d_x = EXTRA ? s2n * Gb[tri(N - 1, N - 1)] + (M::decayed(N - 1) ? wd : 0.0) + damping : 0.0;
+    double y_x = EXTRA ? g[b * N + N - 1] : 0.0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
+    for (int j = 0; j < NC; ++j) {
       Pb[c] = col[j];                           // A[c][j] (= col[j] by symmetry); rows >= j read
       Pb[c == j ? YS : YS + 1] = y;             // y_j is final: the forward solve rides along
-                                                // (slot 33: the other lanes' unconditional store)
+                                                // (slot YS + 1: the other lanes' unconditional store)
+      if constexpr (EXTRA) Pb[c == j ? XS : XS + 1] = col[N - 1];   // A[bias][j]
       wave_lds_sync();
       const double dj = Pb[j];
       double ij = __builtin_amdgcn_rcp(dj);     // 1/d_j: v_rcp_f64 + two Newton steps
@@ -357,18 +369,31 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
       ij = fma(ij, fma(-dj, ij, 1.0), ij);
       if (c == j) dinv_own = ij;
       const double f = c > j ? col[j] * ij : 0.0;
-      y = fma(-f, Pb[YS], y);                   // L y = g, column j
+      const double yj = Pb[YS];
+      y = fma(-f, yj, y);                       // L y = g, column j
       // fixed trip count: the inner loop unrolls before the outer one, so a j-dependent
       // bound would leave col[] indexed at run time (scratch)
 #pragma unroll
-      for (int r = 0; r < N; ++r)
+      for (int r = 0; r < NC; ++r)
         if (r > j) col[r] = fma(-Pb[r], f, col[r]);
+      if constexpr (EXTRA) {
+        const double ax = Pb[XS];
+        col[N - 1] = fma(-ax, f, col[N - 1]);
+        const double lx = ax * ij;              // L[bias][j]
+        d_x = fma(-lx, ax, d_x);
+        y_x = fma(-lx, yj, y_x);
+      }
       if (c > j) col[j] = f;
       wave_lds_sync();                          // this step's reads before the next writes
     }
     y *= dinv_own;
+    if constexpr (EXTRA) {                      // bias solution, then its column of L^T
+      const double xx = y_x / d_x;
+      y = fma(-col[N - 1] * dinv_own, xx, y);
+      if (lane == 0) v[b * N + N - 1] = xx;
+    }
 #pragma unroll
-    for (int j = N - 1; j >= 0; --j) {        // L^T x = D^-1 y
+    for (int j = NC - 1; j >= 0; --j) {       // L^T x = D^-1 y
       const double xj = bcast_col<N>(y, j);
       if (c < j) y = fma(-col[j] * dinv_own, xj, y);
     }
@@ -530,7 +555,7 @@ __global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t
       }
       continue;
     }
-    if constexpr (M::Ds <= 64) {
+    if constexpr (M::Ds <= 65) {
       solve_blocks_regs<M>(Gu, Gi, s2n, A.wd, A.damping, g, v, H, pv);
     } else {
       // block b: H_b = (2/n) Gram_b + wd on decayed coordinates + damping, column-major
