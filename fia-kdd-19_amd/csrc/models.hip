@@ -1511,11 +1511,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
 }
 
 // ------------------------------------------------------------------------------------
-// MF entity-shared scoring with the work item's 256 ratings as 4 rows per lane and the
-// embedding walked 8 coordinates at a time: each 16-B LDS broadcast of a query's x feeds
-// 8 FMAs (4 rows x 2), where k_score_grouped's one row per lane at k >= 64 spent one LDS
-// read per FMA.  Same arithmetic order (and bits) as k_score_grouped; one candidate
-// slot set per work item (spc = 1).
+// MF k >= 32 entity-shared scoring with the query vectors read through the scalar cache.
+// The work item (<= 256 ratings of one entity's list x <= 8 queries sharing the entity)
+// needs, per query, x (k doubles) and a few header words -- the same for every lane.  In
+// LDS every use is a broadcast read that still costs the LDS a full 64-lane transfer
+// (with 4 rows per lane: one 16-B read per 8 FMAs, ~the LDS bandwidth of a CU); here they
+// are s_load'ed into SGPRs and consumed as the SGPR operand of v_fma_f64, leaving LDS
+// idle (20M MF k=64: 5.04 -> 4.74 ms per batch).  One candidate slot set per work item
+// (spc = 1).
 // ------------------------------------------------------------------------------------
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
@@ -1523,12 +1526,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf && M::K % 8 == 0, "MF, k a multiple of 8");
-  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 8;
-  constexpr int RSW = (4 + M::SB + 1) & ~1;      // staged record words, even: 16-B aligned x chunks
+  static_assert(!M::ncf && M::K % 4 == 0, "MF, k a multiple of 4");
+  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4;
   constexpr int NSV = (K + 1 + 63) / 64;
-  __shared__ double srec[kScoreThreads / 64][QB * RSW];
-  __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_items = wstart[nE];
@@ -1555,21 +1555,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
       selfv[v] = c < K ? (double)Es[(int64_t)e * K + c] : (double)Bs[e];
     }
 #define SV(c) readlane_d(selfv[(c) / 64], (c) % 64)
-    double* __restrict__ rl = srec[wave];
-    int64_t* __restrict__ bl = sbase[wave];
-    __builtin_amdgcn_wave_barrier();
-    for (int t = lane; t < QB * RSW; t += 64) {
-      const int j = t / RSW, c = t - j * RSW;
-      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
-      rl[t] = c < 4 + M::SB ? rec[(int64_t)q * M::R + (c < 4 ? c : 4 + sd * M::SB + (c - 4))] : 0.0;
-    }
-    if (lane < QB) {
-      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
-      const int64_t* qb = qbase + 4 * (int64_t)q;
-      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
-      bl[QB + lane] = qb[2 + sd] + cidx;
-      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;
-    }
     int32_t o_[RT], row_[RT];
     float y_[RT], gb_[RT];
     bool ok_[RT];
@@ -1582,21 +1567,20 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
       y_[r] = rat[li];
       row_[r] = rw[li];
     }
-#pragma unroll
-    for (int r = 0; r < RT; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
     const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
     const float* __restrict__ bt = sd == 0 ? A.t[3] : A.t[2];
 #pragma unroll
     for (int r = 0; r < RT; ++r) gb_[r] = bt[o_[r]];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // NQ = nq rounded up to a power of two: a static query count per path keeps the
-    // accumulators in registers without per-query exits (padding columns score copies of
-    // the last query and are never written out).  The embedding chunk of the next step is
-    // gathered while this step's FMAs run.
+    // accumulators in registers (padding columns repeat the last query, never written out)
     auto run = [&](auto nq_c) {
       constexpr int NQ = decltype(nq_c)::value;
+      const double* __restrict__ xq[NQ];        // uniform: this side's x of each query
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
+        xq[j] = rec + (int64_t)q * M::R + 4 + sd * M::SB;
+      }
       double ea[RT], acc[NQ][RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
@@ -1604,43 +1588,37 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
 #pragma unroll
         for (int j = 0; j < NQ; ++j) acc[j][r] = 0.0;
       }
-      auto gather = [&](int c0, float (&g)[RT][CK]) {
+      float4 ga[RT];
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + c0);
-          const float4 a = src[0], b = src[1];
-          g[r][0] = a.x; g[r][1] = a.y; g[r][2] = a.z; g[r][3] = a.w;
-          g[r][4] = b.x; g[r][5] = b.y; g[r][6] = b.z; g[r][7] = b.w;
-        }
-      };
-      float ga[RT][CK];
-      gather(0, ga);
+      for (int r = 0; r < RT; ++r) ga[r] = *reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
 #pragma unroll 1
       for (int c0 = 0; c0 < K; c0 += CK) {
-        float gn[RT][CK];
-        gather(c0 + CK < K ? c0 + CK : c0, gn);
+        float4 gn[RT];
+        const int cn = c0 + CK < K ? c0 + CK : c0;
+#pragma unroll
+        for (int r = 0; r < RT; ++r) gn[r] = *reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + cn);
+        double gd[RT][CK];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          gd[r][0] = ga[r].x; gd[r][1] = ga[r].y; gd[r][2] = ga[r].z; gd[r][3] = ga[r].w;
+        }
 #pragma unroll
         for (int cc = 0; cc < CK; ++cc) {
           const double sc = SV(c0 + cc);
 #pragma unroll
-          for (int r = 0; r < RT; ++r) ea[r] = fma(sc, (double)ga[r][cc], ea[r]);
+          for (int r = 0; r < RT; ++r) ea[r] = fma(sc, gd[r][cc], ea[r]);
         }
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
-          const double2* __restrict__ xr = reinterpret_cast<const double2*>(rl + j * RSW + 4 + K + c0);
 #pragma unroll
-          for (int c2 = 0; c2 < CK / 2; ++c2) {
-            const double2 x2 = xr[c2];
+          for (int cc = 0; cc < CK; ++cc) {
+            const double xc = xq[j][K + c0 + cc];  // scalar load, SGPR operand
 #pragma unroll
-            for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.x, (double)ga[r][2 * c2], acc[j][r]);
-#pragma unroll
-            for (int r = 0; r < RT; ++r) acc[j][r] = fma(x2.y, (double)ga[r][2 * c2 + 1], acc[j][r]);
+            for (int r = 0; r < RT; ++r) acc[j][r] = fma(xc, gd[r][cc], acc[j][r]);
           }
         }
 #pragma unroll
-        for (int r = 0; r < RT; ++r)
-#pragma unroll
-          for (int cc = 0; cc < CK; ++cc) ga[r][cc] = gn[r][cc];
+        for (int r = 0; r < RT; ++r) ga[r] = gn[r];
       }
       {
         const double gbias = (double)A.t[4][0];
@@ -1651,10 +1629,13 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
 #pragma unroll
       for (int j = 0; j < NQ; ++j) {
         if (j >= nq) continue;
-        const double* __restrict__ Rj = rl + j * RSW;
-        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
-        const double xsb = Rj[4 + 2 * K + 1], dup_o = Rj[4 + 2 * K + 2];
-        const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
+        const int32_t q = gq[gb + j];
+        const double* __restrict__ R = rec + (int64_t)q * M::R;
+        const double inv_n = R[0], cq = R[1], xv = R[2], rhat_ui = R[3];
+        const double xsb = xq[j][2 * K + 1], dup_o = xq[j][2 * K + 2];
+        const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
+        const int64_t obj = qb[sd] + (int64_t)cidx * kChunk, cbj = qb[2 + sd] + cidx;
+        const int64_t poj = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
         double la[RT], lv[RT];
         int lp[RT];
 #pragma unroll
@@ -1700,7 +1681,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     else if (nq <= 4) run(std::integral_constant<int, 4>{});
     else run(std::integral_constant<int, QB>{});
 #undef SV
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
