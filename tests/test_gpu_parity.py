@@ -331,3 +331,38 @@ def test_prepare_for_subset(model, k, tmp_path):
         assert np.array_equal(part["x"][j], full["x"][q])
     with pytest.raises(FIAError):
         m.get_influence_batch([11], K=1)
+
+
+@pytest.mark.parametrize("model,k", [("MF", 16), ("NCF", 8), ("MF", 32)])
+def test_many_queries_scan_windows(model, k, tmp_path):
+    """40,000 queries (157 scan tiles of 256: the decoupled look-back walks more than one
+    64-tile window) with repeated users and items: offsets = deg(u) + deg(i) exactly, the
+    related lists and top-K are consistent, and a sample matches the oracle."""
+    from oracle import fia_oracle as fo
+    rng = np.random.default_rng(7 + k)
+    U, I, N = 2000, 300, 30000
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = synth.mf_params(U, I, k, 5) if model == "MF" else synth.ncf_params(U, I, k, 5)
+    Q = 40000
+    qu = rng.integers(0, U, Q).astype(np.int32)
+    qi = rng.integers(0, I, Q).astype(np.int32)
+    m = make_model(model, U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    res = m.get_influence_batch(list(range(Q)), K=2)
+    deg_u = np.bincount(tu, minlength=U)
+    deg_i = np.bincount(ti, minlength=I)
+    assert np.array_equal(np.diff(res["offsets"]), deg_u[qu] + deg_i[qi])
+    assert res["offsets"][0] == 0
+    offs, rel, infl = res["offsets"], res["rel_idx"], res["influence"]
+    for q in rng.choice(Q, 30, replace=False):
+        b, e = offs[q], offs[q + 1]
+        du = deg_u[qu[q]]
+        assert (tu[rel[b:b + du]] == qu[q]).all() and (ti[rel[b + du:e]] == qi[q]).all()
+        assert np.array_equal(res["topk_pos"][q], fo.topk(infl[b:e], 2))
+    for q in rng.choice(Q, 6, replace=False):
+        o = fo.query(model, p, k, tu, ti, tr, int(qu[q]), int(qi[q]), 1e-3, 1e-6)
+        b, e = offs[q], offs[q + 1]
+        assert np.array_equal(o["rel"], rel[b:e])
+        if o["n"]:
+            assert rel_err(infl[b:e], o["influence"]) < RTOL, (model, k, q)
