@@ -1701,9 +1701,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(M::ncf && M::K % 4 == 0, "NCF, k a multiple of 4");
   constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4;
-  constexpr int RSW = (4 + M::SB + 1) & ~1;      // staged record words, even: 16-B aligned x chunks
-  __shared__ __attribute__((aligned(16))) double srec[kScoreThreads / 64][QB * RSW];
-  __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_items = wstart[nE];
@@ -1724,21 +1721,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     const int32_t* __restrict__ rw = A.row[sd] + lb;
     const double* __restrict__ gml = A.lgm[sd] + lb;
     const double* __restrict__ res = A.lres + (int64_t)sd * N + lb;
-    double* __restrict__ rl = srec[wave];
-    int64_t* __restrict__ bl = sbase[wave];
-    __builtin_amdgcn_wave_barrier();
-    for (int t = lane; t < QB * RSW; t += 64) {
-      const int j = t / RSW, c = t - j * RSW;
-      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
-      rl[t] = c < 4 + M::SB ? rec[(int64_t)q * M::R + (c < 4 ? c : 4 + sd * M::SB + (c - 4))] : 0.0;
-    }
-    if (lane < QB) {
-      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
-      const int64_t* qb = qbase + 4 * (int64_t)q;
-      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
-      bl[QB + lane] = qb[2 + sd] + cidx;
-      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
-    }
     int32_t o_[RT], row_[RT], li_[RT];
     float y_[RT];
     double ej[RT];
@@ -1754,14 +1736,17 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
       ej[r] = res[li_[r]];
     }
     const float* __restrict__ T = sd == 0 ? A.t[3] : A.t[2];    // other side's gmf table
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // NQ = nq rounded up to a power of two: a static query count per path, so the
     // accumulators stay in registers without per-query exits (the padding columns
     // score copies of the last query and are never written out)
     auto run = [&](auto nq_c) {
       constexpr int NQ = decltype(nq_c)::value;
+      const double* __restrict__ xq[NQ];        // uniform: this side's record block of each query
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
+        xq[j] = rec + (int64_t)q * M::R + 4 + sd * M::SB;
+      }
       double acc[NQ][RT];
 #pragma unroll
       for (int j = 0; j < NQ; ++j)
@@ -1784,17 +1769,17 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
         }
 #pragma unroll
         for (int j = 0; j < NQ; ++j) {
-          const double2* __restrict__ xm = reinterpret_cast<const double2*>(rl + j * RSW + 4 + c0);
-          const double2* __restrict__ xg = reinterpret_cast<const double2*>(rl + j * RSW + 4 + K + c0);
 #pragma unroll
           for (int c2 = 0; c2 < CK / 2; ++c2) {
-            const double2 a = xm[c2], b = xg[c2];
+            // scalar loads: x_mlp and W3g * x_gmf as SGPR operands (no LDS)
+            const double ax = xq[j][c0 + 2 * c2], ay = xq[j][c0 + 2 * c2 + 1];
+            const double bx = xq[j][K + c0 + 2 * c2], by = xq[j][K + c0 + 2 * c2 + 1];
 #pragma unroll
             for (int r = 0; r < RT; ++r) {
-              acc[j][r] = fma(a.x, gm_[r][2 * c2], acc[j][r]);
-              acc[j][r] = fma(a.y, gm_[r][2 * c2 + 1], acc[j][r]);
-              acc[j][r] = fma(b.x, (double)go_[r][2 * c2], acc[j][r]);
-              acc[j][r] = fma(b.y, (double)go_[r][2 * c2 + 1], acc[j][r]);
+              acc[j][r] = fma(ax, gm_[r][2 * c2], acc[j][r]);
+              acc[j][r] = fma(ay, gm_[r][2 * c2 + 1], acc[j][r]);
+              acc[j][r] = fma(bx, (double)go_[r][2 * c2], acc[j][r]);
+              acc[j][r] = fma(by, (double)go_[r][2 * c2 + 1], acc[j][r]);
             }
           }
         }
@@ -1802,10 +1787,13 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
 #pragma unroll
       for (int j = 0; j < NQ; ++j) {
         if (j >= nq) continue;   // padding columns (copies of the last query)
-        const double* __restrict__ Rj = rl + j * RSW;
+        const int32_t q = gq[gb + j];
+        const double* __restrict__ Rj = rec + (int64_t)q * M::R;
         const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
-        const double dup_o = Rj[4 + 2 * K];
-        const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
+        const double dup_o = xq[j][2 * K];
+        const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
+        const int64_t obj = qb[sd] + (int64_t)cidx * kChunk, cbj = qb[2 + sd] + cidx;
+        const int64_t poj = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
         double la[RT], lv[RT];
         int lp[RT];
 #pragma unroll
