@@ -323,19 +323,24 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
   // hoist N column addresses and N lane masks out of the caller's query loop (spills)
   int lane = threadIdx.x;
   asm volatile("" : "+v"(lane));
-  // both cached blocks into LDS with coalesced loads; the per-lane column reads below are
-  // strided (A[r][c] for r < c sits in row c of the packed lower layout)
-  for (int t = lane; t < GS; t += kSolveThreads) {
-    Hs[t] = Gu[t];
-    Hs[GS + t] = Gi[t];
+  // D_s <= 33: the columns come straight from the cached blocks (L2) -- for a fixed row r
+  // the lanes c < r read consecutive words of packed row r, the lanes c >= r their own row
+  // c (yelp-ex NCF k=16 solve 0.48 -> 0.41 ms); larger blocks are staged through LDS with
+  // coalesced loads first (MF k=64: 1.27 vs 1.49 ms direct)
+  constexpr bool DIRECT = N <= 33;
+  if constexpr (!DIRECT) {
+    for (int t = lane; t < GS; t += kSolveThreads) {
+      Hs[t] = Gu[t];
+      Hs[GS + t] = Gi[t];
+    }
+    __syncthreads();
   }
-  __syncthreads();
 #pragma unroll 1
   for (int b0 = 0; b0 < (PAR ? 1 : 2); ++b0) {
     const int b = PAR ? lane >> 5 : b0;
     const int c = PAR ? lane & 31 : lane;
     const bool live = c < NC;
-    const double* __restrict__ Gb = Hs + b * GS;
+    const double* __restrict__ Gb = DIRECT ? (b ? Gi : Gu) : Hs + b * GS;
     // column slots (one per lane of the block) + y_j + a dummy slot; every lane publishes.
     // PAR: the halves use [0, 34) and [34, 68); otherwise the blocks run in turn on [0, 66)
     // (EXTRA: [0, 68) with the bias row entry at 64 and y_j at 66)
@@ -434,7 +439,7 @@ struct QueryArgs {
 // !COLS: the full D x D packed LDL^T (coupled queries, or every query of qlist).
 // qlist (nullable): {count, q_0, q_1, ...}.
 template <class M, bool COLS>
-__global__ __launch_bounds__(kSolveThreads, 2) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
+__global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
                                                          double* __restrict__ x_out, const int32_t* __restrict__ qlist,
                                                          int32_t* __restrict__ coupled_out) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;

@@ -8,7 +8,7 @@ src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 inc = __import__("os").path.join(__import__("os").path.dirname(__file__), "..", "include")
 out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + inc,
-                      "-c", src, "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"],
+                      "-mllvm", "-pragma-unroll-threshold=200000", "-c", src, "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"],
                      capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
