@@ -1525,6 +1525,13 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
 // idle (20M MF k=64: 5.04 -> 4.74 ms per batch).  One candidate slot set per work item
 // (spc = 1).
 // ------------------------------------------------------------------------------------
+// queries per entity-shared work item: 16 for MF k >= 64, where a work item's gathered
+// rows (256 B each) are the dominant traffic and two query blocks would load them twice
+template <class M>
+constexpr int query_block() {
+  return (!M::ncf && M::K >= 64) ? 16 : kQueryBlock;
+}
+
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
@@ -1532,7 +1539,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && M::K % 4 == 0, "MF, k a multiple of 4");
-  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4;
+  constexpr int K = M::K, RT = kScoreRows, QB = query_block<M>(), CK = 4;
   constexpr int NSV = (K + 1 + 63) / 64;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1684,6 +1691,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     if (nq <= 1) run(std::integral_constant<int, 1>{});
     else if (nq <= 2) run(std::integral_constant<int, 2>{});
     else if (nq <= 4) run(std::integral_constant<int, 4>{});
+    else if (QB == 8 || nq <= 8) run(std::integral_constant<int, 8>{});
     else run(std::integral_constant<int, QB>{});
 #undef SV
   }
@@ -2023,7 +2031,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
-  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, kQueryBlock, s));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, query_block<M>(), s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks

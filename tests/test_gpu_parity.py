@@ -333,7 +333,7 @@ def test_prepare_for_subset(model, k, tmp_path):
         m.get_influence_batch([11], K=1)
 
 
-@pytest.mark.parametrize("model,k", [("MF", 16), ("NCF", 8), ("MF", 32)])
+@pytest.mark.parametrize("model,k", [("MF", 16), ("NCF", 8), ("MF", 32), ("MF", 64)])
 def test_many_queries_scan_windows(model, k, tmp_path):
     """40,000 queries (157 scan tiles of 256: the decoupled look-back walks more than one
     64-tile window) with repeated users and items: offsets = deg(u) + deg(i) exactly, the
