@@ -1895,6 +1895,42 @@ __global__ __launch_bounds__(64) void k_topk_merge(const int32_t* __restrict__ q
   }
 }
 
+// Small K: one THREAD per query walks its chunks' candidates K times (a query has a few to a
+// few hundred candidate slots; a wave per query mostly idles at K = 1).  Same order and
+// output as k_topk_merge.
+__global__ __launch_bounds__(256) void k_topk_merge_thread(
+    const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q, const int64_t* __restrict__ coff,
+    int K, int spc, const int32_t* __restrict__ cand_pos, const double* __restrict__ cand_val,
+    const int64_t* __restrict__ uptr, const int32_t* __restrict__ urow, const int64_t* __restrict__ iptr,
+    const int32_t* __restrict__ irow, int64_t U, int64_t I, int64_t* __restrict__ topk_pos,
+    int64_t* __restrict__ topk_idx, double* __restrict__ topk_val) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  const int64_t cb = coff[q] * spc * K, ce = coff[q + 1] * spc * K;
+  const int32_t u = qu[q], i = qi[q];
+  const bool ok_id = (u >= 0 && u < U && i >= 0 && i < I);
+  const int64_t ub = ok_id ? uptr[u] : 0, du = ok_id ? uptr[u + 1] - ub : 0, ib = ok_id ? iptr[i] : 0;
+  double pa = INFINITY;
+  int pp = -1;
+  for (int t = 0; t < K; ++t) {
+    double ba = -2.0, bv = 0.0;
+    int bp = 0x7fffffff;
+    for (int64_t c = cb; c < ce; ++c) {
+      const int p = cand_pos[c];
+      if (p < 0) continue;
+      const double vv = cand_val[c];
+      const double a = topk_key(vv);
+      if (better(pa, pp, a, p) && better(a, p, ba, bp)) { ba = a; bp = p; bv = vv; }
+    }
+    const bool ok = ba > -1.5;
+    topk_pos[q * K + t] = ok ? bp : -1;
+    topk_idx[q * K + t] = ok ? (int64_t)(bp < du ? urow[ub + bp] : irow[ib + (bp - du)]) : -1;
+    topk_val[q * K + t] = ok ? bv : NAN;
+    pa = ba;
+    pp = bp;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // host-side dispatch
 // ------------------------------------------------------------------------------------
@@ -2083,11 +2119,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   phase_end(c, 2, s);
   if (K > 0 && Q > 0) {
     phase_begin(c, 3, s);
-    hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)Q), dim3(64), 0, s, qu, qi, Q, c->coff.as<int64_t>(), K, spc,
-                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), c->idx.side[0].ptr.as<int64_t>(),
-                       c->idx.side[0].row.as<int32_t>(), c->idx.side[1].ptr.as<int64_t>(),
-                       c->idx.side[1].row.as<int32_t>(), c->p.U, c->p.I, topk_pos, topk_idx, topk_val);
-    FIA_HIP_TRY(hipGetLastError());
+    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, spc, topk_pos, topk_idx, topk_val, s));
     phase_end(c, 3, s);
   }
   return hipSuccess;
@@ -2110,6 +2142,14 @@ bool model_supported(int model, int k) {
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
   if (K <= 0 || Q <= 0) return hipSuccess;
+  if (K <= 4) {
+    hipLaunchKernelGGL(k_topk_merge_thread, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q,
+                       c->coff.as<int64_t>(), K, spc, c->cand_pos.as<int32_t>(), c->cand_val.as<double>(),
+                       c->idx.side[0].ptr.as<int64_t>(), c->idx.side[0].row.as<int32_t>(),
+                       c->idx.side[1].ptr.as<int64_t>(), c->idx.side[1].row.as<int32_t>(), c->p.U, c->p.I, topk_pos,
+                       topk_idx, topk_val);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)Q), dim3(64), 0, s, qu, qi, Q, c->coff.as<int64_t>(), K, spc,
                      c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), c->idx.side[0].ptr.as<int64_t>(),
                      c->idx.side[0].row.as<int32_t>(), c->idx.side[1].ptr.as<int64_t>(),
