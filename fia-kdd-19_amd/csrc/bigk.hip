@@ -1224,7 +1224,7 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   phase_end(c, 2, s);
   if (K > 0) {
     phase_begin(c, 3, s);
-    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, NPASS, topk_pos, topk_idx, topk_val, s));
+    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, NPASS, topk_pos, topk_idx, topk_val, s, max_chunks));
     phase_end(c, 3, s);
   }
   return hipSuccess;

@@ -234,7 +234,8 @@ hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi
                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
-                             int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);
+                             int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
+                             int64_t max_chunks);
 
 // phase event helpers (no-ops unless profiling)
 void phase_begin(fia_ctx* c, int phase, hipStream_t s);

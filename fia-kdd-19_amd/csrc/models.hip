@@ -2119,7 +2119,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   phase_end(c, 2, s);
   if (K > 0 && Q > 0) {
     phase_begin(c, 3, s);
-    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, spc, topk_pos, topk_idx, topk_val, s));
+    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, spc, topk_pos, topk_idx, topk_val, s, max_chunks));
     phase_end(c, 3, s);
   }
   return hipSuccess;
@@ -2140,9 +2140,12 @@ bool model_supported(int model, int k) {
 }
 
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
-                             int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+                             int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
+                             int64_t max_chunks) {
   if (K <= 0 || Q <= 0) return hipSuccess;
-  if (K <= 4) {
+  // a thread per query while the queries have few chunks (<= 16 on average: ml-1m-ex,
+  // yelp-ex); a wave per query over long candidate lists (20M: ~170 chunks per query)
+  if (K <= 4 && max_chunks <= 16 * Q) {
     hipLaunchKernelGGL(k_topk_merge_thread, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q,
                        c->coff.as<int64_t>(), K, spc, c->cand_pos.as<int32_t>(), c->cand_val.as<double>(),
                        c->idx.side[0].ptr.as<int64_t>(), c->idx.side[0].row.as<int32_t>(),
