@@ -298,6 +298,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
+            tj = tj.get(args.config, {}) if "config" not in tj else tj
             if tj.get("config") == args.config and tj.get("kernel", "").startswith(score_kernel(cfg)):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:

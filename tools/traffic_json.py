@@ -1,5 +1,5 @@
 """HBM traffic per dispatch of one kernel from two rocprofv3 PMC passes
-(FETCH_SIZE and WRITE_SIZE, separate runs) -> profiles/score_traffic.json.
+(FETCH_SIZE and WRITE_SIZE, separate runs) -> profiles/score_traffic.json (one entry per config).
 
     python tools/traffic_json.py <config> <kernel-substring> <fetch_dir> <write_dir> <out.json>
 
@@ -24,10 +24,19 @@ def main():
     res = {"config": cfg, "kernel": kern, "hbm_bytes_per_launch": (2 * f + w) * 1024.0,
            "fetch_bytes_per_launch": 2 * f * 1024.0, "write_bytes_per_launch": w * 1024.0,
            "dispatches": [nf, nw],
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (bench.py --steps 5); "
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (short bench.py runs); "
                      "FETCH_SIZE(KB) x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE(KB), x1024, "
                      "per-dispatch average"}
-    json.dump(res, open(out, "w"), indent=2)
+    # one entry per config: {config: {...}} (an older single-entry file is converted)
+    allres = {}
+    if os.path.exists(out):
+        try:
+            old = json.load(open(out))
+            allres = {old["config"]: old} if "config" in old else old
+        except Exception:
+            allres = {}
+    allres[cfg] = res
+    json.dump(allres, open(out, "w"), indent=2)
     print(json.dumps(res))
 
 
