@@ -7,7 +7,8 @@ A step = one pass of the hot path over one batch: per-entity Hessian caches
 batched query (fia_query_batch: exact solve, every related rating's influence
 + train row, top-1 influencer) over the workload's whole query set, all
 resident in HBM.  With N > 1 (torchrun, one rank per GPU) every rank runs the
-same per-GPU batch (weak scaling: the node answers N x the query set) and the
+same-shaped per-GPU batch (weak scaling: rank r > 0 answers the workload's users and
+items re-paired by a seeded permutation, so the node answers N distinct query sets) and the
 step ends with the RCCL all_gather of the top-K influencer lists.
 
 Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (k_score:
@@ -60,6 +61,8 @@ def parse():
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="CPU-baseline worker processes (default: usable host cores, at most 16)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
     return ap.parse_args()
 
@@ -95,34 +98,68 @@ def bytes_per_query(model, k, n):
     return n * (8 * k + 32)
 
 
-def cpu_baseline(cfg, d, params, seconds):
-    """Reference algorithm on the host (1 BLAS thread), RQ1 query order, time-bounded."""
+_CPU = {}     # state the forked CPU-baseline workers inherit
+
+
+def _cpu_worker(w, P, seconds, barrier, out):
     from oracle import ncg_port
-    from influence import synth
     try:
         from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(1)
+        threadpool_limits(1)                      # one BLAS thread per worker process
     except Exception:
-        lim = None
+        pass
+    cfg, d, params, order = _CPU["cfg"], _CPU["d"], _CPU["params"], _CPU["order"]
     tu, ti, tr = d["train"]
     qu, qi, _ = d["test"]
     port = ncg_port.RefAlgorithm(cfg["model"], params, cfg["k"], tu, ti, tr, 1e-3, 1e-6)
-    order = synth.rq1_query_indices(min(100, qu.size), qu.size) if cfg["data"] == "ml1m" else \
-        np.random.default_rng(0).choice(qu.size, min(100, qu.size), replace=False)
+    mine = order[w::P]
+    barrier.wait()
     t0 = time.time()
     done = 0
-    for t in order:
+    for t in mine:
         port.get_influence_on_test_loss(int(qu[t]), int(qi[t]))
         done += 1
         if time.time() - t0 > seconds and done >= 3:
             break
-    dt = time.time() - t0
-    if lim is not None:
-        lim.unregister() if hasattr(lim, "unregister") else None
-    return dict(value=done / dt, unit="queries/s", cores=1, kind="port",
-                sample="%d %s queries in %.1f s (reference algorithm: np.where scans + scipy fmin_ncg "
-                       "avextol=1e-3 maxiter=100 with the verbose callback + per-rating gradient loop)"
-                       % (done, "RQ1-order" if cfg["data"] == "ml1m" else "random", dt))
+    out.put((done, time.time() - t0))
+
+
+def cpu_cores():
+    """Host cores this process may use, capped at the GPU box's CPU share (16 per GPU)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(cfg, d, params, seconds, procs):
+    """Reference algorithm on the host: `procs` query-parallel worker processes, one
+    BLAS thread each, queries dealt round-robin in RQ1 order, time-bounded.  Runs before the
+    process touches the GPU (the workers are forked)."""
+    import multiprocessing as mp
+    from influence import synth
+    qu = d["test"][0]
+    # the whole test set in RQ1 order (np.random.choice without replacement is prefix-stable,
+    # so the first 100 are the RQ1 queries); random order for the synthetic sets
+    order = synth.rq1_query_indices(qu.size, qu.size) if cfg["data"] == "ml1m" else \
+        np.random.default_rng(0).permutation(qu.size)
+    _CPU.update(cfg=cfg, d=d, params=params, order=order)
+    ctx = mp.get_context("fork")
+    barrier, out = ctx.Barrier(procs), ctx.Queue()
+    ws = [ctx.Process(target=_cpu_worker, args=(w, procs, seconds, barrier, out)) for w in range(procs)]
+    for p in ws:
+        p.start()
+    res = [out.get() for _ in ws]
+    for p in ws:
+        p.join()
+    done = sum(r[0] for r in res)
+    dt = max(r[1] for r in res)
+    return dict(value=done / dt, unit="queries/s", cores=procs, kind="port",
+                sample="%d %s queries in %.1f s on %d worker processes x 1 BLAS thread (reference algorithm: "
+                       "np.where scans + scipy fmin_ncg avextol=1e-3 maxiter=100 with the verbose callback + "
+                       "per-rating gradient loop); %.1f queries/s per core"
+                       % (done, "RQ1-order" if cfg["data"] == "ml1m" else "random", dt, procs, done / dt / procs))
 
 
 def main():
@@ -137,23 +174,31 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+
+    d, params = load_data(cfg)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before anything touches the GPU: the baseline's workers are forked from this process
+        cpu = cpu_baseline(cfg, d, params, args.cpu_baseline_seconds, args.cpu_procs or cpu_cores())
     torch.cuda.set_device(dev)
 
     from influence import _lib
     from influence.sharding import TopKGather, shard_ranges
 
-    d, params = load_data(cfg)
     tu, ti, tr = d["train"]
     qu_np, qi_np, _ = d["test"]
+    if world > 1 and rank > 0 and args.shard_of <= 1:
+        # weak scaling with distinct units: rank r > 0 answers its own query set of the same
+        # shape -- the same users and items re-paired by a seeded permutation (new (u, i)
+        # pairs, same per-user / per-item query counts, so the same kind of work per GPU)
+        perm = np.random.default_rng(1000 + rank).permutation(qi_np.size)
+        qi_np = np.ascontiguousarray(qi_np[perm])
     if args.query_order == "item":
         # item-major order (ties by user): queries of one item land in the same batch, so the
         # entity-shared scoring loads a long item list once per <= 8 of them.  Per-query
         # results do not depend on the order.
         order = np.lexsort((qu_np, qi_np))
         qu_np, qi_np = np.ascontiguousarray(qu_np[order]), np.ascontiguousarray(qi_np[order])
-    if world > 1 and rank > 0 and args.shard_of <= 1:   # same per-GPU batch, rank-rotated order
-        shift = (rank * qu_np.size) // world
-        qu_np, qi_np = np.roll(qu_np, -shift), np.roll(qi_np, -shift)
     U, I, k = d["U"], d["I"], cfg["k"]
     model_id = _lib.FIA_MODEL_MF if cfg["model"] == "MF" else _lib.FIA_MODEL_NCF
 
@@ -172,7 +217,7 @@ def main():
     qi = torch.from_numpy(qi_np).to(dev)
     offsets_all, _ = ctx.count_related(qu, qi)
     n_q = np.diff(offsets_all.cpu().numpy())
-    all_sizes = [int(n_q.size)] * world        # weak scaling: every rank answers one full set
+    all_sizes = [int(n_q.size)] * world        # weak scaling: every rank answers one full-size set
     if args.shard_of > 1:
         rs = shard_ranges(n_q, args.shard_of)
         all_sizes = [rs[r % args.shard_of][1] - rs[r % args.shard_of][0] for r in range(world)]
@@ -323,8 +368,8 @@ def main():
         "phases_ms_per_step": {p: (v[0] / max(v[1], 1)) for p, v in phases.items()},
         "index_build_s": index_s,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, d, params, args.cpu_baseline_seconds)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
