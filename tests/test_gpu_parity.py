@@ -366,3 +366,33 @@ def test_many_queries_scan_windows(model, k, tmp_path):
         assert np.array_equal(o["rel"], rel[b:e])
         if o["n"]:
             assert rel_err(infl[b:e], o["influence"]) < RTOL, (model, k, q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [32, 64])
+@pytest.mark.parametrize("K", [1, 4, 6])
+def test_mf_entity_shared_topk_paths(k, K, tmp_path):
+    """MF k >= 32 entity-shared scoring (k_score_grouped_mf) at K = 1, 4, 6: many queries
+    per entity (query blocks split), a query whose pair is a train row; every query's
+    related set, influence and top-K against the fp64 oracle."""
+    from oracle import fia_oracle as fo
+    rng = np.random.default_rng(11 * k + K)
+    U, I, N = 400, 12, 2500
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = synth.mf_params(U, I, k, 9)
+    Q = 300
+    qu = rng.integers(0, U, Q).astype(np.int32)
+    qi = rng.integers(0, I, Q).astype(np.int32)
+    qu[0], qi[0] = tu[17], ti[17]          # pair in train (dup path)
+    m = make_model("MF", U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    res = m.get_influence_batch(list(range(Q)), K=K)
+    offs = res["offsets"]
+    for q in range(Q):
+        o = fo.query("MF", p, k, tu, ti, tr, int(qu[q]), int(qi[q]), 1e-3, 1e-6)
+        b, e = offs[q], offs[q + 1]
+        assert np.array_equal(o["rel"], res["rel_idx"][b:e])
+        assert rel_err(res["influence"][b:e], o["influence"]) < RTOL, (k, K, q)
+        assert np.array_equal(res["topk_pos"][q][:min(K, e - b)], fo.topk(res["influence"][b:e], K)), (k, K, q)
+        check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], K)
