@@ -1158,9 +1158,20 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
   const double* __restrict__ part = sd ? part1 : part0;
   double* __restrict__ gram = sd ? gram1 : gram0;
   const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
+  // partials summed in slot order (deterministic), their loads issued 8 slots at a time
+  // rather than one dependent round trip per slot
   for (int t = threadIdx.x; t < GS; t += 64) {
+    const double* __restrict__ pt = part + (int64_t)first * GSP + t;
     double s = 0.0;
-    for (int k = 0; k < ns; ++k) s += part[(int64_t)(first + k) * GSP + t];
+    int k = 0;
+    for (; k + 8 <= ns; k += 8) {
+      double v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = pt[(int64_t)(k + j) * GSP];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; k < ns; ++k) s += pt[(int64_t)k * GSP];
     gram[(int64_t)e * GSP + t] = s;
   }
 }
@@ -1915,12 +1926,25 @@ __global__ __launch_bounds__(256) void k_topk_merge_thread(
   for (int t = 0; t < K; ++t) {
     double ba = -2.0, bv = 0.0;
     int bp = 0x7fffffff;
-    for (int64_t c = cb; c < ce; ++c) {
+    // both words of a slot loaded unconditionally (empty slots hold -1 / NaN) and 4 slots
+    // per round, so the candidate reads are one round trip per 4 slots, not two per slot
+    int64_t c = cb;
+    for (; c + 4 <= ce; c += 4) {
+      int p4[4];
+      double v4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { p4[j] = cand_pos[c + j]; v4[j] = cand_val[c + j]; }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double a = topk_key(v4[j]);
+        if (p4[j] >= 0 && better(pa, pp, a, p4[j]) && better(a, p4[j], ba, bp)) { ba = a; bp = p4[j]; bv = v4[j]; }
+      }
+    }
+    for (; c < ce; ++c) {
       const int p = cand_pos[c];
-      if (p < 0) continue;
       const double vv = cand_val[c];
       const double a = topk_key(vv);
-      if (better(pa, pp, a, p) && better(a, p, ba, bp)) { ba = a; bp = p; bv = vv; }
+      if (p >= 0 && better(pa, pp, a, p) && better(a, p, ba, bp)) { ba = a; bp = p; bv = vv; }
     }
     const bool ok = ba > -1.5;
     topk_pos[q * K + t] = ok ? bp : -1;
