@@ -729,8 +729,13 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
 
   // right-looking LDL^T: column j holds L[., j], the diagonal holds d
 #pragma unroll
+  // (the diagonal keeps 1/d: v_rcp_f64 + two Newton steps instead of an IEEE division
+  // sequence on the critical path, and the forward solve multiplies by it)
   for (int j = 0; j < Ds; ++j) {
-    const double inv = 1.0 / HS(tri(j, j));
+    const double dj = HS(tri(j, j));
+    double inv = __builtin_amdgcn_rcp(dj);
+    inv = fma(inv, fma(-dj, inv, 1.0), inv);
+    inv = fma(inv, fma(-dj, inv, 1.0), inv);
 #pragma unroll
     for (int r = j + 1; r < Ds; ++r) {
       const double lr = HS(tri(r, j)) * inv;
@@ -739,6 +744,7 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
     }
 #pragma unroll
     for (int r = j + 1; r < Ds; ++r) HS(tri(r, j)) *= inv;
+    HS(tri(j, j)) = inv;
   }
   // v block: user side [q_i ; 1], item side [p_u ; 1]  (gnn:155, mf:194)
   double x[Ds];
@@ -749,7 +755,7 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
 #pragma unroll
     for (int r = j + 1; r < Ds; ++r) x[r] = fma(-HS(tri(r, j)), x[j], x[r]);
 #pragma unroll
-  for (int j = 0; j < Ds; ++j) x[j] /= HS(tri(j, j));
+  for (int j = 0; j < Ds; ++j) x[j] *= HS(tri(j, j));
 #pragma unroll
   for (int j = Ds - 1; j >= 0; --j)
 #pragma unroll
