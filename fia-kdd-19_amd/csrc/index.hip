@@ -116,15 +116,22 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t q0 = tile * kScanTile + (int64_t)threadIdx.x * kScanItems;
   int64_t v[kScanItems];
+  // the list bounds (and the output base) stay in registers for the descriptor fill
+  // after the look-back, instead of a second dependent qu/qi -> ptr round trip
+  int64_t s_ub[kScanItems], s_du[kScanItems], s_ib[kScanItems], s_di[kScanItems], s_base[kScanItems];
   int64_t tsum = 0;
 #pragma unroll
   for (int it = 0; it < kScanItems; ++it) {
     const int64_t q = q0 + it;
     int64_t x = 0;
+    s_ub[it] = s_du[it] = s_ib[it] = s_di[it] = s_base[it] = 0;
     if (q < Q) {
+      if (MODE == 1 && cdesc) s_base[it] = offsets[q];
       const int32_t u = qu[q], i = qi[q];
       if (u >= 0 && u < U && i >= 0 && i < I) {
-        const int64_t du = uptr[u + 1] - uptr[u], di = iptr[i + 1] - iptr[i];
+        const int64_t ub = uptr[u], ib = iptr[i];
+        const int64_t du = uptr[u + 1] - ub, di = iptr[i + 1] - ib;
+        s_ub[it] = ub; s_du[it] = du; s_ib[it] = ib; s_di[it] = di;
         x = MODE == 0 ? du + di : (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
       } else if (MODE == 0) {
         atomicOr(flag + 1, 1);
@@ -189,10 +196,9 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     const int64_t q = q0 + it;
     if (q <= Q) out[q] = run;
     if (MODE == 1 && cdesc && q < Q && v[it] > 0) {
-      int64_t ub, du, ib, di;
-      query_sides(qu, qi, q, uptr, iptr, U, I, ub, du, ib, di);
+      const int64_t ub = s_ub[it], du = s_du[it], ib = s_ib[it], di = s_di[it];
       int64_t c = run;
-      const int64_t base = offsets[q];
+      const int64_t base = s_base[it];
       for (int64_t st = 0; st < du; st += kChunk, ++c) {
         ChunkDesc d;
         d.list_base = ub + st;
