@@ -124,6 +124,25 @@ def _cpu_worker(w, P, seconds, barrier, out):
     out.put((done, time.time() - t0))
 
 
+def rank_query_items(qu, qi, train, I, rank):
+    """Weak scaling with distinct units: rank r > 0 answers its own query set of the same
+    shape -- the workload's users and items re-paired by a seeded permutation (new (u, i)
+    pairs, the same per-user and per-item query counts, so the same related-rating total).
+    Like the real held-out pairs, the new pairs avoid the training set (a pair that is a
+    train row couples the two blocks of its system and takes the full-D solve): colliding
+    entries swap items with random others until none collide.  Returns the new items."""
+    rng = np.random.default_rng(1000 + rank)
+    qi = np.ascontiguousarray(qi[rng.permutation(qi.size)])
+    train_key = np.unique(train[0].astype(np.int64) * int(I) + train[1])
+    for _ in range(64):
+        bad = np.nonzero(np.isin(qu.astype(np.int64) * int(I) + qi, train_key))[0]
+        if bad.size == 0:
+            break
+        for b, o in zip(bad, rng.integers(0, qi.size, bad.size)):
+            qi[b], qi[o] = qi[o], qi[b]
+    return qi
+
+
 def cpu_cores():
     """Host cores this process may use, capped at the GPU box's CPU share (16 per GPU)."""
     try:
@@ -188,11 +207,7 @@ def main():
     tu, ti, tr = d["train"]
     qu_np, qi_np, _ = d["test"]
     if world > 1 and rank > 0 and args.shard_of <= 1:
-        # weak scaling with distinct units: rank r > 0 answers its own query set of the same
-        # shape -- the same users and items re-paired by a seeded permutation (new (u, i)
-        # pairs, same per-user / per-item query counts, so the same kind of work per GPU)
-        perm = np.random.default_rng(1000 + rank).permutation(qi_np.size)
-        qi_np = np.ascontiguousarray(qi_np[perm])
+        qi_np = rank_query_items(qu_np, qi_np, d["train"], d["I"], rank)
     if args.query_order == "item":
         # item-major order (ties by user): queries of one item land in the same batch, so the
         # entity-shared scoring loads a long item list once per <= 8 of them.  Per-query

@@ -74,3 +74,28 @@ def test_gather_topk_gloo_world2(qs):
         assert np.array_equal(gv, want_v)
         assert np.array_equal(gi3, want_i)          # the last async step's lists
         assert np.allclose(gv3, want_v, atol=1e-12)
+
+
+def test_bench_rank_query_sets_are_distinct_and_same_shape():
+    """bench.py weak scaling: rank r > 0 answers re-paired queries -- same users, same item
+    multiset (so the same related-rating total), no pair in train, different from rank 0's."""
+    import importlib
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    bench = importlib.import_module("bench")
+    rng = np.random.default_rng(3)
+    U, I, N, Q = 300, 120, 6000, 900
+    key = rng.choice(U * I, N + Q, replace=False)
+    tu, ti = (key[:N] // I).astype(np.int32), (key[:N] % I).astype(np.int32)
+    qu, qi = (key[N:] // I).astype(np.int32), (key[N:] % I).astype(np.int32)
+    train_key = set((tu.astype(np.int64) * I + ti).tolist())
+    deg_u, deg_i = np.bincount(tu, minlength=U), np.bincount(ti, minlength=I)
+    for rank in (1, 2, 7):
+        q2 = bench.rank_query_items(qu, qi, (tu, ti, None), I, rank)
+        assert np.array_equal(np.sort(q2), np.sort(qi))
+        assert (q2 != qi).mean() > 0.9
+        assert not any(int(u) * I + int(i) in train_key for u, i in zip(qu, q2))
+        assert (deg_u[qu] + deg_i[q2]).sum() == (deg_u[qu] + deg_i[qi]).sum()
