@@ -61,6 +61,8 @@ def parse():
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rank-set", type=int, default=0,
+                    help="answer the query set weak-scaling rank R > 0 answers (check its cost on one GPU)")
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU-baseline worker processes (default: usable host cores, at most 16)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
@@ -128,18 +130,43 @@ def rank_query_items(qu, qi, train, I, rank):
     """Weak scaling with distinct units: rank r > 0 answers its own query set of the same
     shape -- the workload's users and items re-paired by a seeded permutation (new (u, i)
     pairs, the same per-user and per-item query counts, so the same related-rating total).
-    Like the real held-out pairs, the new pairs avoid the training set (a pair that is a
-    train row couples the two blocks of its system and takes the full-D solve): colliding
-    entries swap items with random others until none collide.  Returns the new items."""
+    Like the real held-out pairs, the new pairs are distinct and avoid the training set (a
+    pair that is a train row couples the two blocks of its system and takes the full-D
+    solve): each offending entry swaps items with a random clean entry when both new pairs
+    are clean, until none is left.  Returns the new items."""
     rng = np.random.default_rng(1000 + rank)
-    qi = np.ascontiguousarray(qi[rng.permutation(qi.size)])
-    train_key = np.unique(train[0].astype(np.int64) * int(I) + train[1])
-    for _ in range(64):
-        bad = np.nonzero(np.isin(qu.astype(np.int64) * int(I) + qi, train_key))[0]
-        if bad.size == 0:
+    n, I = qi.size, int(I)
+    qi = np.ascontiguousarray(qi[rng.permutation(n)])
+    tk = np.unique(train[0].astype(np.int64) * I + train[1])
+    qu64 = qu.astype(np.int64)
+
+    def in_train(keys):
+        if tk.size == 0:
+            return np.zeros(keys.shape, bool)
+        pos = np.minimum(np.searchsorted(tk, keys), tk.size - 1)
+        return tk[pos] == keys
+
+    best, stall = n + 1, 0
+    for _ in range(500):
+        keys = qu64 * I + qi
+        bad = in_train(keys)
+        n_train = int(bad.sum())
+        first = np.unique(keys, return_index=True)[1]
+        dup = np.ones(n, bool)
+        dup[first] = False
+        bad |= dup
+        B = np.nonzero(bad)[0]
+        stall = stall + 1 if B.size >= best else 0
+        best = min(best, B.size)
+        # done when clean; a few duplicate pairs among heavy users may stay (harmless)
+        if B.size == 0 or (n_train == 0 and stall >= 20):
             break
-        for b, o in zip(bad, rng.integers(0, qi.size, bad.size)):
-            qi[b], qi[o] = qi[o], qi[b]
+        O = rng.integers(0, n, B.size)
+        ok = ~bad[O] & ~in_train(qu64[B] * I + qi[O]) & ~in_train(qu64[O] * I + qi[B])
+        B, O = B[ok], O[ok]
+        keep = np.unique(O, return_index=True)[1]          # one swap per partner
+        B, O = B[keep], O[keep]
+        qi[B], qi[O] = qi[O], qi[B]
     return qi
 
 
@@ -206,8 +233,9 @@ def main():
 
     tu, ti, tr = d["train"]
     qu_np, qi_np, _ = d["test"]
-    if world > 1 and rank > 0 and args.shard_of <= 1:
-        qi_np = rank_query_items(qu_np, qi_np, d["train"], d["I"], rank)
+    qset = rank if world > 1 else args.rank_set
+    if qset > 0 and args.shard_of <= 1:
+        qi_np = rank_query_items(qu_np, qi_np, d["train"], d["I"], qset)
     if args.query_order == "item":
         # item-major order (ties by user): queries of one item land in the same batch, so the
         # entity-shared scoring loads a long item list once per <= 8 of them.  Per-query

@@ -2113,7 +2113,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          x_out, (const int32_t*)nullptr, c->coupled.as<int32_t>());
     }
     FIA_HIP_TRY(hipGetLastError());
-    const int64_t g2 = Q < 64 ? Q : 64;          // usually no coupled query: a small grid that exits
+    // usually no coupled query: a small grid that exits (a full grid for the large full-D
+    // systems of k >= 32, should many test pairs be train rows)
+    const int64_t gc = M::K <= 16 ? 64 : 256;
+    const int64_t g2 = Q < gc ? Q : gc;
     hipLaunchKernelGGL((k_solve<M, false>), dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
                        x_out, (const int32_t*)c->coupled.as<int32_t>(), (int32_t*)nullptr);
   }
