@@ -1,25 +1,40 @@
 """FIA influence-query throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ml1m-mf|yelp-ncf|20m-mf64]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config ml1m-mf|yelp-ncf|20m-mf64|20m-mf256|20m-ncf256]
 
 A step = one pass of the hot path over one batch: per-entity Hessian caches
-(fia_prepare), related-set counts + offsets (fia_count_related), and the
-batched query (fia_query_batch: exact solve, every related rating's influence
-+ train row, top-1 influencer) over the workload's whole query set, all
-resident in HBM.  With N > 1 (torchrun, one rank per GPU) every rank runs the
-same-shaped per-GPU batch (weak scaling: rank r > 0 answers the workload's users and
-items re-paired by a seeded permutation, so the node answers N distinct query sets) and the
-step ends with the RCCL all_gather of the top-K influencer lists.
+(fia_prepare / fia_prepare_for), related-set counts + offsets (fia_count_related),
+and the batched query (fia_query_batch: exact solve, every related rating's
+influence + train row, top-1 influencer) over the rank's whole query set, all
+resident in HBM.
 
-Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (k_score:
-gather + scoring) by SURVEY.md 8d's algorithmic bytes over its HIP-event
-duration; `cpu_baseline` times the reference ALGORITHM (oracle/ncg_port.py:
-O(N) scans, fmin_ncg with the reference arguments, per-rating gradient loop)
-on a bounded sample on this host.
+Multi-GPU (one process per GPU).  `--gpus N` without a launcher
+re-launches this script under torch.distributed.run with N ranks before anything
+touches the GPU; under torchrun (the driver) WORLD_SIZE/RANK/LOCAL_RANK are read
+from the environment.  Scaling (`--scaling`, default per config):
+  * strong (20M configs): the fixed query set (276,986 held-out pairs) is split into
+    N contiguous ranges balanced by the related-set sizes n_q (influence.sharding.
+    shard_ranges); every rank answers its range;
+  * weak (ml-1m-ex, yelp-ex): every rank answers one full-size query set -- rank 0
+    the workload's own pairs, rank r > 0 the same users and item multiset re-paired
+    by a seeded permutation (distinct pairs, none a training row).
+The only exchange is the RCCL all_gather of the per-query top-K lists, overlapped
+with the next step.  `value` = queries answered by all ranks / the max-over-ranks
+time of the timed steps.
+
+Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (the scoring
+kernel): `achieved` = its HBM bytes per launch measured by rocprofv3 PMC
+(FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction; profiles/
+score_traffic.json) over its HIP-event duration in this run, `frac` = achieved /
+8 TB/s; SURVEY 8d's algorithmic byte count sits beside it under `algorithmic`.
+`cpu_baseline` times the reference ALGORITHM (oracle/ncg_port.py) on a bounded
+sample on this host, with two more CPU figures under `variants`.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -32,41 +47,68 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 
 CONFIGS = {
-    "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m"),
-    "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp"),
+    "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m",
+                    scaling="weak"),
+    "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp",
+                     scaling="weak"),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
-                     k=64, data="20m"),
+                     k=64, data="20m", scaling="strong"),
     "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "
-                      "blocks per query)", model="MF", k=256, data="20m"),
+                      "blocks per query)", model="MF", k=256, data="20m", scaling="strong"),
     "20m-ncf256": dict(workload="NCF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 512^2 "
-                       "blocks per query)", model="NCF", k=256, data="20m"),
+                       "blocks per query)", model="NCF", k=256, data="20m", scaling="strong"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="ml1m-mf", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
+                    help="N > 1: strong = split the fixed query set over the ranks, weak = a full set per rank "
+                         "(auto: strong for the 20M configs, weak otherwise)")
     ap.add_argument("--query-order", default="item", choices=["item", "given"],
                     help="order in which the query set is batched (item-major or the data's order)")
     ap.add_argument("--topk", type=int, default=1)
     ap.add_argument("--batch-rows", type=int, default=1 << 29,
                     help="max related ratings per fia_query_batch call (output buffers are reused)")
     ap.add_argument("--shard-of", type=int, default=1,
-                    help="answer only this rank's 1/S share of the query set (contiguous, balanced by n_q): "
-                         "with S=8 at N=1 this is one GPU's share of the 8-GPU strong-scaling job")
+                    help="answer only shard 0 of S of the strong-scaling split (with S=8 at N=1: one GPU's share "
+                         "of the 8-GPU job)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rank-set", type=int, default=0,
                     help="answer the query set weak-scaling rank R > 0 answers (check its cost on one GPU)")
     ap.add_argument("--cpu-procs", type=int, default=0,
                     help="CPU-baseline worker processes (default: usable host cores, at most 16)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="auto: nccl (RCCL) when every rank has a GPU of its own, gloo when ranks share one")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """--gpus N > 1 outside a launcher: run this script under torch.distributed.run with N
+    ranks (a child process, started before this process touches the GPU) and return its
+    exit code; None when this process is already a rank (or N == 1)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def load_data(cfg):
@@ -82,18 +124,21 @@ def load_data(cfg):
     return d, params
 
 
-def score_kernel(cfg):
+def score_kernel(cfg, K=1):
     """The library's scoring kernel for this config (models.hip / bigk.hip schedule choice)."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_big_score"
     if model == "NCF":
         return "k_score_ncf"
-    return "k_score_mf" if k <= 16 else "k_score_grouped_mf"
+    if k <= 16:
+        return "k_score_mf"
+    return "k_score_grouped_mf"
 
 
 def bytes_per_query(model, k, n):
-    """SURVEY.md 8d algorithmic bytes per query: MF n(4k+32) + 8k+8; NCF n(8k+32)."""
+    """SURVEY.md 8d algorithmic bytes per query: MF n(4k+32) + 8k+8; NCF n(8k+32).  Counts the
+    gathered rows once per query (the entity-shared kernels load them once per query block)."""
     n = np.asarray(n, np.float64)
     if model == "MF":
         return n * (4 * k + 32) + 8 * k + 8
@@ -103,71 +148,53 @@ def bytes_per_query(model, k, n):
 _CPU = {}     # state the forked CPU-baseline workers inherit
 
 
-def _cpu_worker(w, P, seconds, barrier, out):
-    from oracle import ncg_port
+def _cpu_worker(kind, w, P, seconds, barrier, out, blas_threads):
     try:
         from threadpoolctl import threadpool_limits
-        threadpool_limits(1)                      # one BLAS thread per worker process
+        threadpool_limits(blas_threads)
     except Exception:
         pass
-    cfg, d, params, order = _CPU["cfg"], _CPU["d"], _CPU["params"], _CPU["order"]
-    tu, ti, tr = d["train"]
-    qu, qi, _ = d["test"]
-    port = ncg_port.RefAlgorithm(cfg["model"], params, cfg["k"], tu, ti, tr, 1e-3, 1e-6)
-    mine = order[w::P]
+    qu, qi, _ = _CPU["d"]["test"]
+    algo = _CPU["port"] if kind == "port" else _CPU["exact"]
+    mine = _CPU["order"][w::P]
     barrier.wait()
     t0 = time.time()
     done = 0
     for t in mine:
-        port.get_influence_on_test_loss(int(qu[t]), int(qi[t]))
+        if kind == "port":
+            algo.get_influence_on_test_loss(int(qu[t]), int(qi[t]))
+        else:
+            algo.query(int(qu[t]), int(qi[t]))
         done += 1
-        if time.time() - t0 > seconds and done >= 3:
+        if time.time() - t0 > seconds:
             break
     out.put((done, time.time() - t0))
 
 
-def rank_query_items(qu, qi, train, I, rank):
-    """Weak scaling with distinct units: rank r > 0 answers its own query set of the same
-    shape -- the workload's users and items re-paired by a seeded permutation (new (u, i)
-    pairs, the same per-user and per-item query counts, so the same related-rating total).
-    Like the real held-out pairs, the new pairs are distinct and avoid the training set (a
-    pair that is a train row couples the two blocks of its system and takes the full-D
-    solve): each offending entry swaps items with a random clean entry when both new pairs
-    are clean, until none is left.  Returns the new items."""
-    rng = np.random.default_rng(1000 + rank)
-    n, I = qi.size, int(I)
-    qi = np.ascontiguousarray(qi[rng.permutation(n)])
-    tk = np.unique(train[0].astype(np.int64) * I + train[1])
-    qu64 = qu.astype(np.int64)
+def _cpu_run(kind, procs, seconds, blas_threads):
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    barrier, out = ctx.Barrier(procs), ctx.Queue()
+    ws = [ctx.Process(target=_cpu_worker, args=(kind, w, procs, seconds, barrier, out, blas_threads))
+          for w in range(procs)]
+    for p in ws:
+        p.start()
+    res = [out.get() for _ in ws]
+    for p in ws:
+        p.join()
+    done = sum(r[0] for r in res)
+    dt = max(r[1] for r in res)
+    return done, dt
 
-    def in_train(keys):
-        if tk.size == 0:
-            return np.zeros(keys.shape, bool)
-        pos = np.minimum(np.searchsorted(tk, keys), tk.size - 1)
-        return tk[pos] == keys
 
-    best, stall = n + 1, 0
-    for _ in range(500):
-        keys = qu64 * I + qi
-        bad = in_train(keys)
-        n_train = int(bad.sum())
-        first = np.unique(keys, return_index=True)[1]
-        dup = np.ones(n, bool)
-        dup[first] = False
-        bad |= dup
-        B = np.nonzero(bad)[0]
-        stall = stall + 1 if B.size >= best else 0
-        best = min(best, B.size)
-        # done when clean; a few duplicate pairs among heavy users may stay (harmless)
-        if B.size == 0 or (n_train == 0 and stall >= 20):
-            break
-        O = rng.integers(0, n, B.size)
-        ok = ~bad[O] & ~in_train(qu64[B] * I + qi[O]) & ~in_train(qu64[O] * I + qi[B])
-        B, O = B[ok], O[ok]
-        keep = np.unique(O, return_index=True)[1]          # one swap per partner
-        B, O = B[keep], O[keep]
-        qi[B], qi[O] = qi[O], qi[B]
-    return qi
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
 
 
 def cpu_cores():
@@ -180,52 +207,146 @@ def cpu_cores():
 
 
 def cpu_baseline(cfg, d, params, seconds, procs):
-    """Reference algorithm on the host: `procs` query-parallel worker processes, one
-    BLAS thread each, queries dealt round-robin in RQ1 order, time-bounded.  Runs before the
-    process touches the GPU (the workers are forked)."""
-    import multiprocessing as mp
+    """CPU figures on this host, all forked before the
+    process touches the GPU, each time-bounded (at least one query per worker):
+      headline -- the reference ALGORITHM (np.where scans, scipy fmin_ncg with the reference
+                  arguments and verbose callback, per-rating gradient loop; oracle/ncg_port.py)
+                  on `procs` query-parallel processes x 1 BLAS thread;
+      variants -- the same algorithm in ONE process with `procs` BLAS threads, and the
+                  vectorized exact fp64 solve over a CSR index (oracle.CsrExact) on `procs`
+                  processes."""
     from influence import synth
+    from oracle import ncg_port, fia_oracle
+    tu, ti, tr = d["train"]
     qu = d["test"][0]
     # the whole test set in RQ1 order (np.random.choice without replacement is prefix-stable,
     # so the first 100 are the RQ1 queries); random order for the synthetic sets
     order = synth.rq1_query_indices(qu.size, qu.size) if cfg["data"] == "ml1m" else \
         np.random.default_rng(0).permutation(qu.size)
-    _CPU.update(cfg=cfg, d=d, params=params, order=order)
-    ctx = mp.get_context("fork")
-    barrier, out = ctx.Barrier(procs), ctx.Queue()
-    ws = [ctx.Process(target=_cpu_worker, args=(w, procs, seconds, barrier, out)) for w in range(procs)]
-    for p in ws:
-        p.start()
-    res = [out.get() for _ in ws]
-    for p in ws:
-        p.join()
-    done = sum(r[0] for r in res)
-    dt = max(r[1] for r in res)
-    return dict(value=done / dt, unit="queries/s", cores=procs, kind="port",
+    _CPU.update(d=d, order=order,
+                port=ncg_port.RefAlgorithm(cfg["model"], params, cfg["k"], tu, ti, tr, 1e-3, 1e-6),
+                exact=fia_oracle.CsrExact(cfg["model"], params, cfg["k"], tu, ti, tr, 1e-3, 1e-6))
+    sample = "RQ1-order" if cfg["data"] == "ml1m" else "random"
+    done, dt = _cpu_run("port", procs, seconds, 1)
+    head = dict(value=done / dt, unit="queries/s", cores=procs, kind="port", cpu=cpu_model(),
                 sample="%d %s queries in %.1f s on %d worker processes x 1 BLAS thread (reference algorithm: "
                        "np.where scans + scipy fmin_ncg avextol=1e-3 maxiter=100 with the verbose callback + "
-                       "per-rating gradient loop); %.1f queries/s per core"
-                       % (done, "RQ1-order" if cfg["data"] == "ml1m" else "random", dt, procs, done / dt / procs))
+                       "per-rating gradient loop, oracle/ncg_port.py); %.2f queries/s per core"
+                       % (done, sample, dt, procs, done / dt / procs))
+    var = []
+    s2 = max(3.0, seconds / 2)
+    done, dt = _cpu_run("port", 1, s2, procs)
+    var.append(dict(name="reference algorithm, 1 process x %d BLAS threads" % procs, value=done / dt,
+                    unit="queries/s", cores=procs, sample="%d %s queries in %.1f s" % (done, sample, dt)))
+    done, dt = _cpu_run("exact", procs, s2, 1)
+    var.append(dict(name="exact fp64 solve + vectorized scoring over a CSR index (oracle.CsrExact), "
+                         "%d processes x 1 BLAS thread" % procs, value=done / dt, unit="queries/s", cores=procs,
+                    sample="%d %s queries in %.1f s" % (done, sample, dt)))
+    head["variants"] = var
+    return head
+
+
+def rank_query_items(qu, qi, train, I, rank, stats=None):
+    """Weak scaling with distinct units: rank r > 0 answers its own query set of the same
+    shape -- the workload's users and items re-paired by a seeded permutation (new (u, i)
+    pairs, the same per-user and per-item query counts, so the same related-rating total).
+    Like the real held-out pairs, the new pairs are distinct and avoid the training set (a
+    pair that is a train row couples the two blocks of its system and takes the full-D
+    solve): each offending entry swaps items with a random clean entry when both new pairs
+    are clean, until none is left.  Returns the new items; `stats` (a dict) receives the
+    pairs still in train / duplicated if the swaps could not remove them all."""
+    rng = np.random.default_rng(1000 + rank)
+    n, I = qi.size, int(I)
+    qi = np.ascontiguousarray(qi[rng.permutation(n)])
+    tk = np.unique(train[0].astype(np.int64) * I + train[1])
+    qu64 = qu.astype(np.int64)
+
+    def in_train(keys):
+        if tk.size == 0:
+            return np.zeros(keys.shape, bool)
+        pos = np.minimum(np.searchsorted(tk, keys), tk.size - 1)
+        return tk[pos] == keys
+
+    def duplicated(keys):
+        first = np.unique(keys, return_index=True)[1]
+        dup = np.ones(n, bool)
+        dup[first] = False
+        return dup
+
+    best, stall = n + 1, 0
+    for _ in range(500):
+        keys = qu64 * I + qi
+        bad = in_train(keys)
+        n_train = int(bad.sum())
+        bad |= duplicated(keys)
+        B = np.nonzero(bad)[0]
+        stall = stall + 1 if B.size >= best else 0
+        best = min(best, B.size)
+        # done when clean; a few duplicate pairs among heavy users may stay (harmless)
+        if B.size == 0 or (n_train == 0 and stall >= 20):
+            break
+        O = rng.integers(0, n, B.size)
+        ok = ~bad[O] & ~in_train(qu64[B] * I + qi[O]) & ~in_train(qu64[O] * I + qi[B])
+        B, O = B[ok], O[ok]
+        keep = np.unique(O, return_index=True)[1]          # one swap per partner
+        B, O = B[keep], O[keep]
+        qi[B], qi[O] = qi[O], qi[B]
+    keys = qu64 * I + qi
+    left_train, left_dup = int(in_train(keys).sum()), int(duplicated(keys).sum())
+    if left_train:
+        print("bench: rank %d query set keeps %d training pairs (full-D coupled solves)" % (rank, left_train),
+              file=sys.stderr)
+    if stats is not None:
+        stats.update(train_pairs=left_train, duplicate_pairs=left_dup)
+    return qi
+
+
+def load_traffic(path, config, kernel):
+    """PMC HBM bytes per launch of `kernel` for `config` (profiles/score_traffic.json), or None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        tj = json.load(open(path))
+        tj = tj.get(config, {}) if "config" not in tj else tj
+        if tj.get("config") == config and tj.get("kernel", "").startswith(kernel):
+            return tj
+    except Exception:
+        return None
+    return None
 
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
     cfg = CONFIGS[args.config]
+    scaling = cfg["scaling"] if args.scaling == "auto" else args.scaling
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if world > 1 and args.gpus not in (1, world):
+        print("bench: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
 
     d, params = load_data(cfg)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before anything touches the GPU: the baseline's workers are forked from this process
         cpu = cpu_baseline(cfg, d, params, args.cpu_baseline_seconds, args.cpu_procs or cpu_cores())
+
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    backend = args.dist_backend
+    if backend == "auto":
+        backend = "nccl" if world <= ndev else "gloo"
+    if world > 1:
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(dev)
 
     from influence import _lib
@@ -233,19 +354,20 @@ def main():
 
     tu, ti, tr = d["train"]
     qu_np, qi_np, _ = d["test"]
-    qset = rank if world > 1 else args.rank_set
+    repair = {}
+    qset = rank if (world > 1 and scaling == "weak") else args.rank_set
     if qset > 0 and args.shard_of <= 1:
-        qi_np = rank_query_items(qu_np, qi_np, d["train"], d["I"], qset)
+        qi_np = rank_query_items(qu_np, qi_np, d["train"], d["I"], qset, repair)
     if args.query_order == "item":
         # item-major order (ties by user): queries of one item land in the same batch, so the
-        # entity-shared scoring loads a long item list once per <= 8 of them.  Per-query
+        # entity-shared scoring loads a long item list once per query block.  Per-query
         # results do not depend on the order.
         order = np.lexsort((qu_np, qi_np))
         qu_np, qi_np = np.ascontiguousarray(qu_np[order]), np.ascontiguousarray(qi_np[order])
     U, I, k = d["U"], d["I"], cfg["k"]
     model_id = _lib.FIA_MODEL_MF if cfg["model"] == "MF" else _lib.FIA_MODEL_NCF
 
-    ctx = _lib.Context(local)
+    ctx = _lib.Context(dev.index)
     names = list(params)
     tables = [torch.from_numpy(np.ascontiguousarray(params[n], np.float32)).to(dev) for n in names]
     ctx.set_params(model_id, k, U, I, tables, 1e-3, 1e-6)
@@ -260,13 +382,18 @@ def main():
     qi = torch.from_numpy(qi_np).to(dev)
     offsets_all, _ = ctx.count_related(qu, qi)
     n_q = np.diff(offsets_all.cpu().numpy())
-    all_sizes = [int(n_q.size)] * world        # weak scaling: every rank answers one full-size set
-    if args.shard_of > 1:
-        rs = shard_ranges(n_q, args.shard_of)
-        all_sizes = [rs[r % args.shard_of][1] - rs[r % args.shard_of][0] for r in range(world)]
-        b0, b1 = rs[rank % args.shard_of]
+    # this rank's queries and every rank's count
+    if scaling == "strong" and (world > 1 or args.shard_of > 1):
+        S = world if world > 1 else args.shard_of
+        rs = shard_ranges(n_q, S)
+        all_sizes = [b - a for a, b in rs][:world] if world > 1 else [rs[0][1] - rs[0][0]]
+        b0, b1 = rs[rank if world > 1 else 0]
         qu_np, qi_np, n_q = qu_np[b0:b1], qi_np[b0:b1], n_q[b0:b1]
         qu, qi = qu[b0:b1].contiguous(), qi[b0:b1].contiguous()
+        shard_of = S
+    else:
+        all_sizes = [int(n_q.size)] * world
+        shard_of = 1
     Q = int(qu_np.size)
     total = int(n_q.sum())
     D = ctx.num_params()
@@ -284,19 +411,21 @@ def main():
         qb_u, qb_i = qu[b0:b1], qi[b0:b1]
         off_b, tot_b = ctx.count_related(qb_u, qb_i)
         batches.append((b0, b1, qb_u, qb_i, off_b, tot_b))
-    max_rows = max(b[5] for b in batches)
-    max_q = max(b[1] - b[0] for b in batches)
+    max_rows = max([b[5] for b in batches] + [1])
+    max_q = max([b[1] - b[0] for b in batches] + [1])
     rel = torch.empty(max_rows, dtype=torch.int64, device=dev)
     infl = torch.empty(max_rows, dtype=torch.float64, device=dev)
     xbuf = torch.empty(max_q * D, dtype=torch.float64, device=dev)
-    tp = torch.empty(Q * K, dtype=torch.int64, device=dev)
-    tix = torch.empty(Q * K, dtype=torch.int64, device=dev)
-    tv = torch.empty(Q * K, dtype=torch.float64, device=dev)
+    tp = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev)
+    tix = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev)
+    tv = torch.empty(max(Q * K, 1), dtype=torch.float64, device=dev)
 
     big_k = k >= 128 or (cfg["model"] == "NCF" and k >= 64)
 
-    # the top-K exchange: one async all_gather per step, overlapped with the next step
-    tg = TopKGather(all_sizes, K, dev) if world > 1 else None
+    # the top-K exchange: one async all_gather per step, overlapped with the next step (gloo:
+    # host copies of the lists, for rehearsals with several ranks on one GPU)
+    gdev = dev if backend == "nccl" else torch.device("cpu")
+    tg = TopKGather(all_sizes, K, gdev) if world > 1 else None
 
     def compute():
         if big_k:
@@ -308,13 +437,16 @@ def main():
             ctx.query_batch(qb_u, qb_i, off_b, tot_b, rel, infl, xbuf, K, tp[b0 * K:b1 * K],
                             tix[b0 * K:b1 * K], tv[b0 * K:b1 * K])
 
-    def step():
-        compute()
+    def exchange():
         if tg is not None:
-            tg.start(tix.view(Q, K), tv.view(Q, K))
+            a, b = tix[:Q * K].view(Q, K), tv[:Q * K].view(Q, K)
+            if gdev.type == "cpu":
+                a, b = a.cpu(), b.cpu()
+            tg.start(a, b)
 
     for _ in range(args.warmup):
-        step()
+        compute()
+        exchange()
     if tg is not None:
         tg.wait()
     torch.cuda.synchronize(dev)
@@ -322,15 +454,15 @@ def main():
     # below record only the scoring phase's event pair (the roofline kernel time)
     ctx.profile_read()
     ctx.set_profiling(True)
-    for _ in range(min(args.steps, 5)):
+    n_instr = max(1, min(args.steps, 5))
+    for _ in range(n_instr):
         compute()
     torch.cuda.synchronize(dev)
     ctx.set_profiling(False)
     phases = ctx.profile_read()
-    # the timed steps: the whole step (prepare + related counts + query batches) captured
-    # once as a HIP graph and replayed -- every kernel still runs every step; the graph only
-    # removes host launch cost and inter-kernel gaps.  fia_prepare_for (large k) decides
-    # the cache size on the host, so those configs run eagerly.
+    # optional: the whole step captured once as a HIP graph and replayed (every kernel still
+    # runs every step; the graph only removes host launch cost).  fia_prepare_for (large k)
+    # decides the cache size on the host, so those configs run eagerly.
     use_graph = args.graph and not big_k
     graph = None
     if use_graph:
@@ -345,21 +477,17 @@ def main():
             compute()
         torch.cuda.synchronize(dev)
 
-    def timed_step():
-        if graph is not None:
-            graph.replay()
-        else:
-            compute()
-        if tg is not None:
-            tg.start(tix.view(Q, K), tv.view(Q, K))
-
     ctx.set_profiling(True, phases=("score",))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        timed_step()
+        if graph is not None:
+            graph.replay()
+        else:
+            compute()
+        exchange()
     if tg is not None:
         tg.wait()
     torch.cuda.synchronize(dev)
@@ -369,48 +497,51 @@ def main():
     ctx.set_profiling(False)
     timed = ctx.profile_read()          # scoring kernel duration over the timed region
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
     ms_per_step = elapsed * 1e3 / args.steps
-    value = world * Q * args.steps / elapsed
+    node_queries = int(sum(all_sizes))
+    value = node_queries * args.steps / elapsed
     score_ms = timed["score"][0] / max(timed["score"][1], 1)            # per launch, timed region
     if timed["score"][1] == 0:
         # graph replay: the library's events are not re-recorded by a replayed graph, so the
         # kernel time comes from the instrumented eager steps
         score_ms = phases["score"][0] / max(phases["score"][1], 1)
-    bytes_launch = float(bytes_per_query(cfg["model"], k, n_q).sum()) / len(batches)   # mean per launch
-    achieved = bytes_launch / (score_ms * 1e-3) / 1e9
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            tj = tj.get(args.config, {}) if "config" not in tj else tj
-            if tj.get("config") == args.config and tj.get("kernel", "").startswith(score_kernel(cfg)):
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
+    kern = score_kernel(cfg, K)
+    alg_bytes = float(bytes_per_query(cfg["model"], k, n_q).sum()) / len(batches)   # mean per launch
+    tj = load_traffic(args.traffic_json, args.config, kern)
+    traffic = tj.get("hbm_bytes_per_launch") if tj else None
+    achieved = traffic / (score_ms * 1e-3) / 1e9 if traffic else None
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
+                "kernel": kern, "kernel_ms": score_ms,
+                "source": ("rocprofv3 PMC (FETCH_SIZE x 2 + WRITE_SIZE) per launch, %s" % os.path.relpath(
+                    args.traffic_json, ROOT)) if traffic else "no PMC traffic recorded for this config/kernel",
+                "algorithmic": {"model": "SURVEY.md 8d (gathered rows counted once per query)",
+                                "bytes_per_launch": alg_bytes, "gbs": alg_bytes / (score_ms * 1e-3) / 1e9}}
     out = {
         "metric": "influence queries/sec (whole node) + % HBM roofline, MF k=16 ML-1M-ex"
         if args.config == "ml1m-mf" else "influence queries/sec (whole node), " + cfg["workload"],
         "value": value, "unit": "queries/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak" if args.shard_of <= 1 else "strong", "vs_baseline": None,
+        "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic train ratings of the reference shape (train file not distributed) + the reference's "
-                "real held-out test pairs; synthetic parameters",
-        "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_gpu": Q,
-                   "n_train": int(tu.size), "related_ratings_per_gpu_step": int(total), "topk": K,
-                   "query_batches": len(batches), "query_order": args.query_order, "shard_of": args.shard_of,
-                   "hip_graph": use_graph,
+                "real held-out test pairs (20M: synthetic held-out pairs); synthetic parameters",
+        "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_rank": all_sizes,
+                   "node_queries_per_step": node_queries, "n_train": int(tu.size),
+                   "related_ratings_rank0_step": int(total), "topk": K, "query_batches": len(batches),
+                   "query_order": args.query_order, "shard_of": shard_of, "hip_graph": use_graph,
+                   "dist_backend": backend if world > 1 else None,
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": score_kernel(cfg), "kernel_ms": score_ms, "algorithmic_bytes_per_launch": bytes_launch},
-        "phases_ms_per_step": {p: (v[0] / max(v[1], 1)) for p, v in phases.items()},
+        "roofline": roofline,
+        "phases_ms_per_step": {p: v[0] / n_instr for p, v in phases.items()},
+        "phases_ms_per_launch": {p: (v[0] / max(v[1], 1)) for p, v in phases.items()},
         "index_build_s": index_s,
     }
+    if repair:
+        out["config"]["rank0_requery"] = repair
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -97,28 +97,29 @@ int fia_destroy(fia_ctx* c) {
     DeviceGuard g(c->device);
     (void)hipDeviceSynchronize();
     for (int s = 0; s < 2; ++s) {
-      c->idx.side[s].ptr.release();
-      c->idx.side[s].row.release();
-      c->idx.side[s].other.release();
-      c->idx.side[s].rating.release();
-      c->gram[s].release();
-      c->l1[s].release();
-      c->idx.order[s].release();
-      c->idx.gitems[s].release();
-      c->idx.gcomb[s].release();
-      c->gpart[s].release();
-      c->self[s].release();
-      c->gm[s].release();
-      c->slot[s].release();
-      c->bitems[s].release();
-      c->bcomb[s].release();
+      c->idx.side[s].ptr.release(nullptr);
+      c->idx.side[s].row.release(nullptr);
+      c->idx.side[s].other.release(nullptr);
+      c->idx.side[s].rating.release(nullptr);
+      c->gram[s].release(nullptr);
+      c->l1[s].release(nullptr);
+      c->idx.order[s].release(nullptr);
+      c->idx.gitems[s].release(nullptr);
+      c->idx.gcomb[s].release(nullptr);
+      c->gpart[s].release(nullptr);
+      c->self[s].release(nullptr);
+      c->gm[s].release(nullptr);
+      c->slot[s].release(nullptr);
+      c->bitems[s].release(nullptr);
+      c->bcomb[s].release(nullptr);
     }
-    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->scan_tmp, &c->qscan,
+    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->qscan,
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
-                           &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->wcnt,
+                           &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->gscan,
                            &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,
                            &c->cpllist, &c->lscr, &c->mark};
-    for (auto* b : bufs) b->release();
+    for (auto* b : bufs) b->release(nullptr);
+    (void)hipDeviceSynchronize();   // the stream-ordered frees complete before the context goes
     for (auto& v : c->events.ev)
       for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto e : c->events.pool) (void)hipEventDestroy(e);
@@ -241,7 +242,7 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     hipStream_t s = as_stream(stream);
     hipError_t e;
     if (total_out) {
-      e = c->flag.reserve(64);
+      e = c->flag.reserve(64, s);
       if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
       e = hipMemsetAsync(c->flag.ptr, 0, 64, s);
       if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");

@@ -1051,7 +1051,7 @@ int cu_count(fia_ctx* c) {
 // slot -dst-1 of a split list; split lists get a combine entry {cache slot, first partial,
 // n partials, 0} summed in slot order.  marks == nullptr: every entity, slot = entity id
 // (lists cached per index); else only the marked entities, numbered in entity order.
-hipError_t big_work_lists(fia_ctx* c, const std::vector<uint8_t>* marks) {
+hipError_t big_work_lists(fia_ctx* c, const std::vector<uint8_t>* marks, hipStream_t s) {
   Index& X = c->idx;
   if (!marks && !c->subset && c->bitems_version == X.version) return hipSuccess;
   for (int sd = 0; sd < 2; ++sd) {
@@ -1080,17 +1080,18 @@ hipError_t big_work_lists(fia_ctx* c, const std::vector<uint8_t>* marks) {
     c->n_bslots[sd] = parts;
     c->n_bcache[sd] = ncache;
     if (!items.empty()) {
-      FIA_HIP_TRY(c->bitems[sd].reserve(sizeof(int32_t) * items.size()));
-      FIA_HIP_TRY(hipMemcpy(c->bitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+      FIA_HIP_TRY(c->bitems[sd].reserve(sizeof(int32_t) * items.size(), s));
+      FIA_HIP_TRY(hipMemcpyAsync(c->bitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice, s));
     }
     if (!comb.empty()) {
-      FIA_HIP_TRY(c->bcomb[sd].reserve(sizeof(int32_t) * comb.size()));
-      FIA_HIP_TRY(hipMemcpy(c->bcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
+      FIA_HIP_TRY(c->bcomb[sd].reserve(sizeof(int32_t) * comb.size(), s));
+      FIA_HIP_TRY(hipMemcpyAsync(c->bcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice, s));
     }
     if (marks) {
-      FIA_HIP_TRY(c->slot[sd].reserve(sizeof(int32_t) * (size_t)(ne + 1)));
-      FIA_HIP_TRY(hipMemcpy(c->slot[sd].ptr, slot.data(), sizeof(int32_t) * slot.size(), hipMemcpyHostToDevice));
+      FIA_HIP_TRY(c->slot[sd].reserve(sizeof(int32_t) * (size_t)(ne + 1), s));
+      FIA_HIP_TRY(hipMemcpyAsync(c->slot[sd].ptr, slot.data(), sizeof(int32_t) * slot.size(), hipMemcpyHostToDevice, s));
     }
+    FIA_HIP_TRY(hipStreamSynchronize(s));   // this side's host lists are freed at the end of the iteration
   }
   c->bitems_version = marks ? ~0ull : X.version;
   c->subset = marks != nullptr;
@@ -1108,7 +1109,7 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
   // entity selection first (host round trip), so a too-large cache fails before any work
   std::vector<uint8_t> marks[2];
   if (qu) {
-    FIA_HIP_TRY(c->mark.reserve((size_t)(n_ent[0] + n_ent[1])));
+    FIA_HIP_TRY(c->mark.reserve((size_t)(n_ent[0] + n_ent[1]), s));
     FIA_HIP_TRY(hipMemsetAsync(c->mark.ptr, 0, (size_t)(n_ent[0] + n_ent[1]), s));
     if (Q > 0) {
       hipLaunchKernelGGL(k_mark, dim3(grid_cap((Q + 255) / 256, 4096)), dim3(256), 0, s, Q, qu, qi, n_ent[0],
@@ -1122,9 +1123,9 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
                                hipMemcpyDeviceToHost, s));
     FIA_HIP_TRY(hipStreamSynchronize(s));
   }
-  FIA_HIP_TRY(big_work_lists(c, qu ? marks : nullptr));
+  FIA_HIP_TRY(big_work_lists(c, qu ? marks : nullptr, s));
   FIA_HIP_TRY(ensure_self(c, s));
-  FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(N + 1)));
+  FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(N + 1), s));
   if constexpr (!M::ncf) {
     if (N > 0) {
       hipLaunchKernelGGL(k_resid_mf<K>, dim3(gN), dim3(256), 0, s, N, c->self[0].as<int32_t>(),
@@ -1134,11 +1135,11 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
     }
   } else {
     for (int sd = 0; sd < 2; ++sd) {
-      FIA_HIP_TRY(c->l1[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * K + 1)));
+      FIA_HIP_TRY(c->l1[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * K + 1), s));
       hipLaunchKernelGGL(k_l1_big<K>, dim3(grid_cap((n_ent[sd] * K + 255) / 256, 16384)), dim3(256), 0, s,
                          c->p.t[sd], c->p.t[4], sd * K, n_ent[sd], c->l1[sd].as<double>());
       FIA_HIP_TRY(hipGetLastError());
-      FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1)));
+      FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1), s));
     }
     if (N > 0) {
       hipLaunchKernelGGL(k_ncf_rows<K>, dim3(grid_cap((N + 15) / 16, 65536)), dim3(64), 0, s, N,
@@ -1151,8 +1152,8 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
     }
   }
   for (int sd = 0; sd < 2; ++sd) {
-    FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)((c->n_bcache[sd] > 0 ? c->n_bcache[sd] : 1) * GW)));
-    if (c->n_bslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(c->n_bslots[sd] * GW)));
+    FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)((c->n_bcache[sd] > 0 ? c->n_bcache[sd] : 1) * GW), s));
+    if (c->n_bslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(c->n_bslots[sd] * GW), s));
     const float* emb_other = M::ncf ? c->p.t[sd == 0 ? 3 : 2] : c->p.t[sd == 0 ? 1 : 0];
     if (c->n_bitems[sd] > 0) {
       hipLaunchKernelGGL(k_big_gram<M>, dim3(grid_cap(c->n_bitems[sd], 1 << 20), GramCfg<M>::NG), dim3(64 * kGW), 0, s,
@@ -1178,7 +1179,7 @@ hipError_t launch_solve(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int
   const int64_t resident = (int64_t)cu_count(c) * (per_cu > 0 ? per_cu : 1);
   const int64_t grid = max_sys < resident ? max_sys : resident;
   constexpr int64_t slab = (int64_t)(NP + 16) * NP;
-  FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(grid * slab)));
+  FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(grid * slab), s));
   hipLaunchKernelGGL((k_big_solve<M, NP, CPL>), dim3((unsigned)grid), dim3(solve_threads<NP>()), 0, s, A, list,
                      c->qwork.as<double>(), c->lscr.as<double>(), c->xb.as<double>(), c->rec.as<double>());
   return hipGetLastError();
@@ -1189,14 +1190,14 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
                           int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
                           int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
   constexpr int NPs = M::NPs, NPASS = kScoreRows, SW = score_waves<M>();
-  FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));
-  FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * M::QW + 1)));
-  FIA_HIP_TRY(c->xb.reserve(sizeof(double) * (size_t)(Q * 2 * NPs + 1)));
-  FIA_HIP_TRY(c->syslist.reserve(sizeof(int32_t) * (size_t)(2 * Q + 2)));
-  FIA_HIP_TRY(c->cpllist.reserve(sizeof(int32_t) * (size_t)(Q + 2)));
+  FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
+  FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * M::QW + 1), s));
+  FIA_HIP_TRY(c->xb.reserve(sizeof(double) * (size_t)(Q * 2 * NPs + 1), s));
+  FIA_HIP_TRY(c->syslist.reserve(sizeof(int32_t) * (size_t)(2 * Q + 2), s));
+  FIA_HIP_TRY(c->cpllist.reserve(sizeof(int32_t) * (size_t)(Q + 2), s));
   if (K > 0) {
-    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * NPASS)));
-    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * NPASS)));
+    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * NPASS), s));
+    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * NPASS), s));
   }
   const BigArgs A = make_big_args(c, qu, qi);
   phase_begin(c, 4, s);
@@ -1242,7 +1243,7 @@ hipError_t ensure_self(fia_ctx* c, hipStream_t s) {
   if (c->self_version == X.version) return hipSuccess;
   const int64_t N = X.N, n_ent[2] = {X.U, X.I};
   for (int sd = 0; sd < 2; ++sd) {
-    FIA_HIP_TRY(c->self[sd].reserve(sizeof(int32_t) * (size_t)(N + 1)));
+    FIA_HIP_TRY(c->self[sd].reserve(sizeof(int32_t) * (size_t)(N + 1), s));
     if (N > 0) {
       hipLaunchKernelGGL(k_self, dim3(grid_cap((N + 255) / 256, 65536)), dim3(256), 0, s, N, n_ent[sd],
                          X.side[sd].ptr.as<int64_t>(), c->self[sd].as<int32_t>());

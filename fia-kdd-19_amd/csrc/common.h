@@ -32,28 +32,32 @@ constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
 constexpr int kBigQueryBlock = 8;        // ... large k (register-resident per-query sums)
 
-// Device buffer with grow-on-demand capacity (never shrinks).
+// Device buffer with grow-on-demand capacity (never shrinks), allocated from the
+// device's stream-ordered pool on the context's stream: growing a buffer frees the old
+// block in stream order (kernels already queued on `s` still read it) and allocates
+// the new one behind them -- no device-wide synchronisation on the query path.  A
+// regrown buffer gets 25 % headroom so a slowly growing batch does not regrow it
+// every call.  Contents are not preserved.
 struct DevBuf {
   void* ptr = nullptr;
   size_t bytes = 0;
-  hipError_t reserve(size_t want) {
-    if (want <= bytes) return hipSuccess;
+  hipError_t reserve(size_t want, hipStream_t s) {
+    if (want <= bytes && ptr) return hipSuccess;
+    size_t cap = want < 256 ? 256 : want;
     if (ptr) {
-      // the old allocation may still be read by queued kernels
-      hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) return e;
-      e = hipFree(ptr);
+      const size_t grown = bytes + bytes / 4;
+      if (grown > cap) cap = grown;
+      hipError_t e = hipFreeAsync(ptr, s);
       if (e != hipSuccess) return e;
       ptr = nullptr;
       bytes = 0;
     }
-    size_t cap = want < 256 ? 256 : want;
-    hipError_t e = hipMalloc(&ptr, cap);
-    if (e == hipSuccess) bytes = cap;
+    hipError_t e = hipMallocAsync(&ptr, cap, s);
+    if (e == hipSuccess) bytes = cap; else ptr = nullptr;
     return e;
   }
-  void release() {
-    if (ptr) (void)hipFree(ptr);
+  void release(hipStream_t s) {
+    if (ptr) (void)hipFreeAsync(ptr, s);
     ptr = nullptr;
     bytes = 0;
   }
@@ -153,20 +157,19 @@ struct fia_ctx {
   fia::DevBuf cdesc;      // ChunkDesc [max chunks]
   fia::DevBuf cand_pos;   // int32 [max chunks * K]
   fia::DevBuf cand_val;   // double [max chunks * K]
-  fia::DevBuf scan_tmp;   // rocprim temporary storage
   fia::DevBuf qscan;      // k_query_scan tile words + counters (left zero by every launch)
   fia::DevBuf flag;       // int32 [4] device status words
   fia::DevBuf nch;        // int64 [Q+1] chunk counts
   fia::DevBuf coupled;    // int32 [Q + 1]: count, then queries whose test pair is a train row
   // query groups per entity (entity-shared scoring): global entity index g = e (users) or
   // U + e (items)
-  fia::DevBuf gcnt;       // int64 [U + I + 1] queries per entity -> exclusive scan in gstart
+  fia::DevBuf gcnt;       // uint64 [U + I + 1] queries per entity -> exclusive scan in gstart
   fia::DevBuf gstart;     // int64 [U + I + 1]
   fia::DevBuf grank;      // int32 [2Q] rank of query q in its user group / item group
   fia::DevBuf gq;         // int32 [2Q] queries grouped by entity (users then items)
   fia::DevBuf qbase;      // int64 [2Q] per query and side: output base, candidate-slot base
-  fia::DevBuf wcnt;       // int64 [U + I + 1] work items per entity -> scan in wstart
-  fia::DevBuf wstart;     // int64 [U + I + 1]
+  fia::DevBuf wstart;     // int64 [U + I + 1] exclusive scan of the work items per entity
+  fia::DevBuf gscan;      // k_group_scan tile words + counters (left zero by every launch)
   fia::DevBuf witems;     // int32 [3 * max items] {global entity, list chunk, query block}
   // large-k path (bigk.hip): per-list-position entity, per-train-row residual / NCF backward
   // vectors, per-query Hessian inputs and solutions, solve lists and LDL^T scratch
@@ -206,9 +209,8 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 // per-query chunk offsets coff (+ chunk descriptors unless offsets_only)
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr);
-hipError_t build_gram_lists(fia_ctx* c, int64_t chunk);
+hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
 int64_t gram_chunk(int64_t want);
-hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_items, int qb, hipStream_t s);

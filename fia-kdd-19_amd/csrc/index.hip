@@ -11,7 +11,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include "common.h"
@@ -100,6 +99,41 @@ __device__ inline void query_sides(const int32_t* qu, const int32_t* qi, int64_t
 constexpr int kScanThreads = 256, kScanItems = 1, kScanTile = kScanThreads * kScanItems;
 constexpr unsigned long long kScanAgg = 1ull << 62, kScanPre = 2ull << 62, kScanVal = (1ull << 62) - 1;
 
+// Wave 0 of a scan block: publish tile `tile`'s aggregate, then look back with the whole
+// wave -- lane l reads the word of tile (window end - l); the nearest inclusive prefix ends
+// the walk -- and publish the tile's inclusive prefix.  Returns the exclusive prefix (in
+// every lane).  Tile words: {flag (2 bits): 1 aggregate / 2 inclusive prefix, value (62 bits)}.
+__device__ int64_t scan_lookback(unsigned long long* __restrict__ tstate, int64_t tile, int64_t agg) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0)
+    __hip_atomic_store(&tstate[tile], (tile == 0 ? kScanPre : kScanAgg) | (unsigned long long)agg,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int64_t excl = 0;
+  for (int64_t end = tile - 1; end >= 0;) {
+    const int64_t p = end - lane;
+    const unsigned long long w =
+        p >= 0 ? __hip_atomic_load(&tstate[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kScanPre;
+    const unsigned long long f = w >> 62;
+    const unsigned long long pre = __ballot(f == 2), inv = __ballot(f == 0);
+    const int stop = pre ? __builtin_ctzll(pre) : 64;            // first lane holding a prefix
+    const unsigned long long need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+    if (inv & need) {                                              // a needed tile not published yet
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    int64_t part = lane <= stop ? (int64_t)(w & kScanVal) : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    excl += part;
+    if (stop < 64) break;
+    end -= 64;
+  }
+  if (lane == 0 && tile > 0)
+    __hip_atomic_store(&tstate[tile], kScanPre | (unsigned long long)(excl + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q, const int64_t* __restrict__ uptr,
@@ -155,36 +189,9 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     if (w < wave) wbase += s_wave[w];
     agg += s_wave[w];
   }
-  // publish this tile's aggregate, then look back with the whole first wave: lane l reads
-  // the word of tile (window end - l); the nearest inclusive prefix ends the walk
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&tstate[tile], (tile == 0 ? kScanPre : kScanAgg) | (unsigned long long)agg,
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (wave == 0) {
-    int64_t excl = 0;
-    for (int64_t end = tile - 1; end >= 0;) {
-      const int64_t p = end - lane;
-      const unsigned long long w =
-          p >= 0 ? __hip_atomic_load(&tstate[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kScanPre;
-      const unsigned long long f = w >> 62;
-      const unsigned long long pre = __ballot(f == 2), inv = __ballot(f == 0);
-      const int stop = pre ? __builtin_ctzll(pre) : 64;            // first lane holding a prefix
-      const unsigned long long need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
-      if (inv & need) {                                              // a needed tile not published yet
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      int64_t part = lane <= stop ? (int64_t)(w & kScanVal) : 0;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-      excl += part;
-      if (stop < 64) break;
-      end -= 64;
-    }
+    const int64_t excl = scan_lookback(tstate, tile, agg);
     if (lane == 0) {
-      if (tile > 0)
-        __hip_atomic_store(&tstate[tile], kScanPre | (unsigned long long)(excl + agg), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
       s_prefix = excl;
       if (MODE == 1 && tile == 0 && zero_word) zero_word[0] = 0;   // solve's coupled-query counter
     }
@@ -259,24 +266,80 @@ __global__ void k_group_count(const int32_t* __restrict__ qu, const int32_t* __r
   qbase[4 * q + 3] = coff[q] + (du + kChunk - 1) / kChunk;
 }
 
-// threads over max(Q, U + I + 1): place queries into their groups; work items per entity
-__global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q,
-                             const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr, int64_t U, int64_t I,
+// thread per query: place it into its user group and its item group
+__global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q, int64_t U,
                              const int64_t* __restrict__ gstart, const int32_t* __restrict__ grank,
-                             const unsigned long long* __restrict__ gcnt, int32_t* __restrict__ gq,
-                             int64_t* __restrict__ wcnt, int qb) {
+                             int32_t* __restrict__ gq) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < Q && grank[2 * t] >= 0) {
     const int32_t u = qu[t], i = qi[t];
     gq[gstart[u] + grank[2 * t]] = (int32_t)t;
     gq[gstart[U + i] + grank[2 * t + 1]] = (int32_t)t;
   }
+}
+
+// Single-pass decoupled look-back scan over the U + I entities (users, then items) of
+// the two per-entity counts of the entity-shared schedule: queries per entity (gcnt ->
+// gstart) and work items per entity, ceil(deg / kChunk) * ceil(gcnt / qb) (-> wstart).
+// Both exclusive prefixes (and the totals at [U + I]) in one launch: no library scan, no
+// count array.  tstate: two arrays of tile words (queries, work items); the last tile to
+// finish re-zeroes them and the two counters.
+__global__ __launch_bounds__(kScanThreads) void k_group_scan(
+    const unsigned long long* __restrict__ gcnt, const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr,
+    int64_t U, int64_t I, int qb, int64_t* __restrict__ gstart, int64_t* __restrict__ wstart,
+    unsigned long long* __restrict__ tstate, unsigned int* __restrict__ tctr) {
+  __shared__ int s_tile;
+  __shared__ int64_t s_wa[kScanThreads / 64], s_wb[kScanThreads / 64];
+  __shared__ int64_t s_pa, s_pb;
   const int64_t nE = U + I;
+  const unsigned ntiles = (unsigned)((nE + 1 + kScanTile - 1) / kScanTile);
+  if (threadIdx.x == 0) s_tile = (int)atomicAdd(&tctr[0], 1u);
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t = tile * kScanTile + threadIdx.x;
+  int64_t a = 0, b = 0;
   if (t < nE) {
-    const int64_t deg = t < U ? uptr[t + 1] - uptr[t] : iptr[t - U + 1] - iptr[t - U];
-    wcnt[t] = gcnt[t] > 0 ? ((deg + kChunk - 1) / kChunk) * (((int64_t)gcnt[t] + qb - 1) / qb) : 0;
-  } else if (t == nE) {
-    wcnt[nE] = 0;
+    a = (int64_t)gcnt[t];
+    if (a > 0) {
+      const int64_t deg = t < U ? uptr[t + 1] - uptr[t] : iptr[t - U + 1] - iptr[t - U];
+      b = ((deg + kChunk - 1) / kChunk) * ((a + qb - 1) / qb);
+    }
+  }
+  int64_t ia = a, ib = b;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t ya = __shfl_up(ia, off), yb = __shfl_up(ib, off);
+    if (lane >= off) { ia += ya; ib += yb; }
+  }
+  if (lane == 63) { s_wa[wave] = ia; s_wb[wave] = ib; }
+  __syncthreads();
+  int64_t ba = 0, bb = 0, agg_a = 0, agg_b = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / 64; ++w) {
+    if (w < wave) { ba += s_wa[w]; bb += s_wb[w]; }
+    agg_a += s_wa[w];
+    agg_b += s_wb[w];
+  }
+  if (wave == 0) {
+    const int64_t ea = scan_lookback(tstate, tile, agg_a);
+    const int64_t eb = scan_lookback(tstate + ntiles, tile, agg_b);
+    if (lane == 0) { s_pa = ea; s_pb = eb; }
+  }
+  __syncthreads();
+  if (t <= nE) {
+    gstart[t] = s_pa + ba + ia - a;
+    wstart[t] = s_pb + bb + ib - b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned done = atomicAdd(&tctr[1], 1u);
+    if (done == ntiles - 1) {
+      for (unsigned w = 0; w < 2 * ntiles; ++w)
+        __hip_atomic_store(&tstate[w], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&tctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&tctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -344,18 +407,10 @@ inline int grid_for(int64_t n, int threads, int cap = 8192) {
 
 }  // namespace
 
-hipError_t exclusive_scan_i64(fia_ctx* c, const int64_t* in, int64_t* out, int64_t n, hipStream_t s) {
-  size_t tb = 0;
-  FIA_HIP_TRY(rocprim::exclusive_scan(nullptr, tb, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), s));
-  FIA_HIP_TRY(c->scan_tmp.reserve(tb + 16));
-  size_t tb2 = c->scan_tmp.bytes;
-  return rocprim::exclusive_scan(c->scan_tmp.ptr, tb2, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), s);
-}
-
 // Small-k Gram work lists of the current index: items of <= chunk list rows {entity,
 // start, len, slot} (longest lists first), slot < 0 = write the Gram directly, else a
 // partial slot; a combine entry {entity, first slot, n slots, 0} per split entity.
-hipError_t build_gram_lists(fia_ctx* c, int64_t chunk) {
+hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s) {
   Index& X = c->idx;
   for (int sd = 0; sd < 2; ++sd) {
     const std::vector<int64_t>& hptr = X.hptr[sd];
@@ -375,13 +430,14 @@ hipError_t build_gram_lists(fia_ctx* c, int64_t chunk) {
     X.n_gcomb[sd] = (int64_t)comb.size() / 4;
     X.n_gslots[sd] = slots;
     if (!items.empty()) {
-      FIA_HIP_TRY(X.gitems[sd].reserve(sizeof(int32_t) * items.size()));
-      FIA_HIP_TRY(hipMemcpy(X.gitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice));
+      FIA_HIP_TRY(X.gitems[sd].reserve(sizeof(int32_t) * items.size(), s));
+      FIA_HIP_TRY(hipMemcpyAsync(X.gitems[sd].ptr, items.data(), sizeof(int32_t) * items.size(), hipMemcpyHostToDevice, s));
     }
     if (!comb.empty()) {
-      FIA_HIP_TRY(X.gcomb[sd].reserve(sizeof(int32_t) * comb.size()));
-      FIA_HIP_TRY(hipMemcpy(X.gcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice));
+      FIA_HIP_TRY(X.gcomb[sd].reserve(sizeof(int32_t) * comb.size(), s));
+      FIA_HIP_TRY(hipMemcpyAsync(X.gcomb[sd].ptr, comb.data(), sizeof(int32_t) * comb.size(), hipMemcpyHostToDevice, s));
     }
+    FIA_HIP_TRY(hipStreamSynchronize(s));   // this side's host lists are freed at the end of the iteration
   }
   X.gchunk = chunk;
   return hipSuccess;
@@ -391,7 +447,7 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
                        const float* rating, hipStream_t s, std::string& why) {
   Index& X = c->idx;
   X.valid = false;
-  FIA_HIP_TRY(c->flag.reserve(64));
+  FIA_HIP_TRY(c->flag.reserve(64, s));
   FIA_HIP_TRY(hipMemsetAsync(c->flag.ptr, 0, 64, s));
   if (N > 0) {
     hipLaunchKernelGGL(k_check_ids, dim3(grid_for(N, 256)), dim3(256), 0, s, user, item, N, U, I,
@@ -406,24 +462,24 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
     return hipErrorInvalidValue;
   }
   DevBuf keys_sorted, tmp;
-  FIA_HIP_TRY(keys_sorted.reserve(sizeof(int32_t) * (size_t)(N > 0 ? N : 1)));
+  FIA_HIP_TRY(keys_sorted.reserve(sizeof(int32_t) * (size_t)(N > 0 ? N : 1), s));
   const int32_t* key_src[2] = {user, item};
   const int32_t* other_src[2] = {item, user};
   int64_t n_ent[2] = {U, I};
   for (int sd = 0; sd < 2; ++sd) {
     Side& S = X.side[sd];
     size_t nb = sizeof(int32_t) * (size_t)(N > 0 ? N : 1);
-    FIA_HIP_TRY(S.row.reserve(nb));
-    FIA_HIP_TRY(S.other.reserve(nb));
-    FIA_HIP_TRY(S.rating.reserve(sizeof(float) * (size_t)(N > 0 ? N : 1)));
-    FIA_HIP_TRY(S.ptr.reserve(sizeof(int64_t) * (size_t)(n_ent[sd] + 1)));
+    FIA_HIP_TRY(S.row.reserve(nb, s));
+    FIA_HIP_TRY(S.other.reserve(nb, s));
+    FIA_HIP_TRY(S.rating.reserve(sizeof(float) * (size_t)(N > 0 ? N : 1), s));
+    FIA_HIP_TRY(S.ptr.reserve(sizeof(int64_t) * (size_t)(n_ent[sd] + 1), s));
     if (N > 0) {
       unsigned eb = bits_for(n_ent[sd]);
       rocprim::counting_iterator<int32_t> iota(0);
       size_t tb = 0;
       FIA_HIP_TRY(rocprim::radix_sort_pairs(nullptr, tb, key_src[sd], keys_sorted.as<int32_t>(), iota,
                                             S.row.as<int32_t>(), (size_t)N, 0u, eb, s));
-      FIA_HIP_TRY(tmp.reserve(tb + 16));
+      FIA_HIP_TRY(tmp.reserve(tb + 16, s));
       tb = tmp.bytes;
       FIA_HIP_TRY(rocprim::radix_sort_pairs(tmp.ptr, tb, key_src[sd], keys_sorted.as<int32_t>(), iota,
                                             S.row.as<int32_t>(), (size_t)N, 0u, eb, s));
@@ -437,26 +493,28 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
     FIA_HIP_TRY(hipStreamSynchronize(s));   // keys_sorted is reused by the next side
     // entities by list length, longest first: the Gram kernels start the long lists early
     std::vector<int64_t> hptr((size_t)n_ent[sd] + 1);
-    FIA_HIP_TRY(hipMemcpy(hptr.data(), S.ptr.ptr, sizeof(int64_t) * hptr.size(), hipMemcpyDeviceToHost));
+    FIA_HIP_TRY(hipMemcpyAsync(hptr.data(), S.ptr.ptr, sizeof(int64_t) * hptr.size(), hipMemcpyDeviceToHost, s));
+    FIA_HIP_TRY(hipStreamSynchronize(s));
     std::vector<int32_t> ord((size_t)n_ent[sd]);
     for (int64_t e = 0; e < n_ent[sd]; ++e) ord[(size_t)e] = (int32_t)e;
     std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
       return hptr[(size_t)a + 1] - hptr[(size_t)a] > hptr[(size_t)b + 1] - hptr[(size_t)b];
     });
     X.hptr[sd] = hptr;
-    FIA_HIP_TRY(X.order[sd].reserve(sizeof(int32_t) * ord.size()));
-    FIA_HIP_TRY(hipMemcpy(X.order[sd].ptr, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice));
+    FIA_HIP_TRY(X.order[sd].reserve(sizeof(int32_t) * ord.size(), s));
+    FIA_HIP_TRY(hipMemcpyAsync(X.order[sd].ptr, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice, s));
+    FIA_HIP_TRY(hipStreamSynchronize(s));
     X.hord[sd] = ord;
   }
-  FIA_HIP_TRY(build_gram_lists(c, gram_chunk(kGramChunk)));
-  keys_sorted.release();
-  tmp.release();
+  FIA_HIP_TRY(build_gram_lists(c, gram_chunk(kGramChunk), s));
+  keys_sorted.release(s);
+  tmp.release(s);
   // pair set, load factor <= 1/2
   int64_t cap = 1024;
   while (cap < 2 * N) cap <<= 1;
-  FIA_HIP_TRY(X.pkey.reserve(sizeof(unsigned long long) * (size_t)cap));
-  FIA_HIP_TRY(X.pcnt.reserve(sizeof(int32_t) * (size_t)cap));
-  FIA_HIP_TRY(X.psum.reserve(sizeof(double) * (size_t)cap));
+  FIA_HIP_TRY(X.pkey.reserve(sizeof(unsigned long long) * (size_t)cap, s));
+  FIA_HIP_TRY(X.pcnt.reserve(sizeof(int32_t) * (size_t)cap, s));
+  FIA_HIP_TRY(X.psum.reserve(sizeof(double) * (size_t)cap, s));
   FIA_HIP_TRY(hipMemsetAsync(X.pkey.ptr, 0xff, sizeof(unsigned long long) * (size_t)cap, s));
   FIA_HIP_TRY(hipMemsetAsync(X.pcnt.ptr, 0, sizeof(int32_t) * (size_t)cap, s));
   FIA_HIP_TRY(hipMemsetAsync(X.psum.ptr, 0, sizeof(double) * (size_t)cap, s));
@@ -482,9 +540,8 @@ static hipError_t scan_state(fia_ctx* c, int64_t Q, hipStream_t s) {
   const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
   const size_t need = sizeof(unsigned long long) * (size_t)ntiles + 16;
   if (c->qscan.bytes >= need && c->qscan.ptr) return hipSuccess;
-  FIA_HIP_TRY(hipStreamSynchronize(s));
-  c->qscan.release();
-  FIA_HIP_TRY(c->qscan.reserve(need < 4096 ? 4096 : need));
+  // stream-ordered regrow (the previous launches on s still own the old block)
+  FIA_HIP_TRY(c->qscan.reserve(need < 4096 ? 4096 : need, s));
   FIA_HIP_TRY(hipMemsetAsync(c->qscan.ptr, 0, c->qscan.bytes, s));
   return hipSuccess;
 }
@@ -493,7 +550,7 @@ template <int MODE>
 static hipError_t launch_query_scan(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* out,
                                     const int64_t* offsets, ChunkDesc* cdesc, int32_t* zero_word, hipStream_t s) {
   FIA_HIP_TRY(scan_state(c, Q, s));
-  FIA_HIP_TRY(c->flag.reserve(64));
+  FIA_HIP_TRY(c->flag.reserve(64, s));
   const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
   unsigned int* ctr = reinterpret_cast<unsigned int*>(c->qscan.as<char>() + c->qscan.bytes - 16);
   hipLaunchKernelGGL(k_query_scan<MODE>, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, qu, qi, Q,
@@ -518,8 +575,8 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word) {
-  FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1)));
-  if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1)));
+  FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1), s));
+  if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
   return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
                               offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s);
 }
@@ -527,14 +584,20 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_items, int qb, hipStream_t s) {
   const int64_t U = c->idx.U, I = c->idx.I, nE = U + I;
-  FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
-  FIA_HIP_TRY(c->gstart.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
-  FIA_HIP_TRY(c->wcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
-  FIA_HIP_TRY(c->wstart.reserve(sizeof(int64_t) * (size_t)(nE + 1)));
-  FIA_HIP_TRY(c->grank.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1)));
-  FIA_HIP_TRY(c->gq.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1)));
-  FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1)));
-  FIA_HIP_TRY(c->witems.reserve(sizeof(int32_t) * (size_t)(3 * max_items + 3)));
+  const int64_t ntiles = (nE + 1 + kScanTile - 1) / kScanTile;
+  FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
+  FIA_HIP_TRY(c->gstart.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
+  FIA_HIP_TRY(c->wstart.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
+  FIA_HIP_TRY(c->grank.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1), s));
+  FIA_HIP_TRY(c->gq.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1), s));
+  FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1), s));
+  FIA_HIP_TRY(c->witems.reserve(sizeof(int32_t) * (size_t)(3 * max_items + 3), s));
+  // k_group_scan state: 2 x ntiles tile words + 2 counters, zero at allocation and left zero
+  const size_t need = sizeof(unsigned long long) * (size_t)(2 * ntiles) + 16;
+  if (c->gscan.bytes < need || !c->gscan.ptr) {
+    FIA_HIP_TRY(c->gscan.reserve(need, s));
+    FIA_HIP_TRY(hipMemsetAsync(c->gscan.ptr, 0, c->gscan.bytes, s));
+  }
   const int64_t* uptr = c->idx.side[0].ptr.as<int64_t>();
   const int64_t* iptr = c->idx.side[1].ptr.as<int64_t>();
   FIA_HIP_TRY(hipMemsetAsync(c->gcnt.ptr, 0, sizeof(int64_t) * (size_t)(nE + 1), s));
@@ -544,13 +607,16 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                        c->qbase.as<int64_t>());
     FIA_HIP_TRY(hipGetLastError());
   }
-  FIA_HIP_TRY(exclusive_scan_i64(c, c->gcnt.as<int64_t>(), c->gstart.as<int64_t>(), nE + 1, s));
-  const int64_t nt = (Q > nE + 1 ? Q : nE + 1);
-  hipLaunchKernelGGL(k_group_fill, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr, U, I,
-                     c->gstart.as<int64_t>(), c->grank.as<int32_t>(), c->gcnt.as<unsigned long long>(),
-                     c->gq.as<int32_t>(), c->wcnt.as<int64_t>(), qb);
+  unsigned int* ctr = reinterpret_cast<unsigned int*>(c->gscan.as<char>() + c->gscan.bytes - 16);
+  hipLaunchKernelGGL(k_group_scan, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, c->gcnt.as<unsigned long long>(),
+                     uptr, iptr, U, I, qb, c->gstart.as<int64_t>(), c->wstart.as<int64_t>(),
+                     c->gscan.as<unsigned long long>(), ctr);
   FIA_HIP_TRY(hipGetLastError());
-  FIA_HIP_TRY(exclusive_scan_i64(c, c->wcnt.as<int64_t>(), c->wstart.as<int64_t>(), nE + 1, s));
+  if (Q > 0) {
+    hipLaunchKernelGGL(k_group_fill, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q, U,
+                       c->gstart.as<int64_t>(), c->grank.as<int32_t>(), c->gq.as<int32_t>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
   hipLaunchKernelGGL(k_item_fill, dim3(grid_for(max_items, 256, 16384)), dim3(256), 0, s, c->wstart.as<int64_t>(),
                      c->gcnt.as<unsigned long long>(), nE, c->witems.as<int32_t>(), qb);
   return hipGetLastError();

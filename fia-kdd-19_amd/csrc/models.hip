@@ -2001,10 +2001,10 @@ template <class M>
 hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   constexpr int Ds = M::Ds, GS = Ds * (Ds + 1) / 2, K = M::K;
   const int64_t n_ent[2] = {c->p.U, c->p.I};
-  for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * ((GS + 1) & ~1) + 1)));
+  for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * ((GS + 1) & ~1) + 1), s));
   if constexpr (M::ncf) {
     for (int sd = 0; sd < 2; ++sd) {
-      FIA_HIP_TRY(c->l1[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * K + 1)));
+      FIA_HIP_TRY(c->l1[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * K + 1), s));
       const int64_t tot = n_ent[sd] * K;
       if (tot > 0) {
         hipLaunchKernelGGL(k_ncf_l1<K>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, c->p.t[sd],
@@ -2021,11 +2021,11 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
     int64_t want = 256;
     while (!M::ncf && want < 4096 && want < GSP) want *= 2;   // NCF: 256 (16 slabs per item)
     want = gram_chunk(want);
-    if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want));
+    if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want, s));
   }
   const Index& X = c->idx;
   for (int sd = 0; sd < 2; ++sd)
-    if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP)));
+    if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP), s));
   GramSides G;
   for (int sd = 0; sd < 2; ++sd) {
     G.n_items[sd] = n_ent[sd] > 0 ? X.n_gitems[sd] : 0;
@@ -2042,8 +2042,8 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   if constexpr (M::ncf) {
     // per list position of each side: g_mlp (coordinate-major) and e, with the Grams
     const int64_t N = X.N;
-    for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1)));
-    FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * N + 1)));
+    for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1), s));
+    FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * N + 1), s));
     for (int sd = 0; sd < 2; ++sd) G.lgm[sd] = c->gm[sd].as<double>();
     const int64_t n_all = G.n_items[0] + G.n_items[1];
     if (n_all > 0) {
@@ -2083,10 +2083,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
   const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
-  FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1)));
+  FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   if (K > 0) {
-    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc)));
-    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * spc)));
+    FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc), s));
+    FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * spc), s));
   }
   QueryArgs A = make_args(c, qu, qi);
   const int64_t nE = c->idx.U + c->idx.I;
@@ -2094,7 +2094,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int64_t max_items = max_chunks;
   // the queries whose test pair is a train row are listed in `coupled` {count, q...} by the
   // solve and finished full-D; the chunk scan zeroes the count
-  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1)));
+  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, query_block<M>(), s));

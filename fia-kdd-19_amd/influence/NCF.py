@@ -48,6 +48,12 @@ class NCF(GenericNeuralNet):
             n[8]: _truncated_normal(rng, (3 * h,), 1.0 / np.sqrt(3 * h)), n[9]: np.zeros(1, np.float32),
         }
 
+    def retrain(self, num_steps, feed_dict):
+        """NCF.retrain (NCF.py:68-72): num_steps Adam steps on mini-batches of self.batch_size
+        drawn by DataSet.next_batch from the feed's rows; unlike MF, the Adam state is NOT
+        reset."""
+        self._retrain_minibatch(num_steps, feed_dict)
+
     def _split_theta(self, x):
         k = self.embedding_size
         return [x[:k], x[k:2 * k], x[2 * k:3 * k], x[3 * k:4 * k]]

@@ -9,23 +9,37 @@ test_retraining is the RQ1 validation harness (experiments.py:17-150,
 SURVEY.md 8f row 2): predicted influence of the top training ratings vs the
 change of r-hat(test) after leave-one-out retraining (influence/train.py).
 """
+import os
+
 import numpy as np
 
 
 def record_time_cost(model, test_idx, iter_to_load=None, force_refresh=False, random_seed=17):
+    """experiments.py:4-15: one FIA query, timed.  The reference returns 0 and prints the
+    three stage timers; this returns them too (model.last_timing: inverse_hvp_s,
+    multiply_s, total_s, wall_s, n)."""
     np.random.seed(random_seed)
     if iter_to_load is not None:
         model.load_checkpoint(iter_to_load)
     approx_params = {"batch_size": model.batch_size, "damping": model.damping}
     model.get_influence_on_test_loss([test_idx], np.arange(len(model.data_sets["train"].labels)),
                                      force_refresh=force_refresh, approx_params=approx_params)
-    return 0
+    return model.last_timing
 
 
-def maxinf(model, test_idx, num_to_remove=1):
+def total_y_diffs_path(model, test_idx):
+    """experiments.py:43: np.save("output/%s-[%s]-_total_y_diffs" % (model_name, test_idx)) --
+    under the model's train_dir (the reference hard-codes output/, its default train_dir)."""
+    return os.path.join(model.train_dir, "%s-[%s]-_total_y_diffs.npy" % (model.model_name, test_idx))
+
+
+def maxinf(model, test_idx, num_to_remove=1, save=True):
     """(predicted_y_diffs[top], indices_to_remove (related positions), train rows), computed
-    on the GPU by the fused top-K of fia_query_batch."""
+    on the GPU by the fused top-K of fia_query_batch.  Like the reference's maxinf branch
+    (experiments.py:36-48) the full predicted vector is saved first (save=True)."""
     res = model.get_influence_batch([test_idx], K=num_to_remove, full=True, return_x=False)
+    if save:
+        np.save(total_y_diffs_path(model, test_idx), res["influence"])
     pos = res["topk_pos"][0]
     keep = pos >= 0
     model.train_indices_of_test_case = res["rel_idx"]

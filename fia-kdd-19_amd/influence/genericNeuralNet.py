@@ -21,6 +21,24 @@ from influence import _lib
 from influence.dataset import DataSet
 
 
+def rq2_timing(phases, n, wall_s, log=None):
+    """The reference's three RQ2 stage timers (mf:224-250: 'Inverse HVP took', 'Multiplying by
+    n train examples took', 'Total time is') from the library's per-phase HIP-event sums
+    (ms, count) of one query call: the inverse HVP is the related-list build ('chunks'), the
+    per-entity Hessian caches if rebuilt ('prepare') and the exact solve ('solve'); the
+    multiplication is the per-rating scoring ('score') and the top-K merge ('topk').
+    Returns dict(inverse_hvp_s, multiply_s, total_s, wall_s, n)."""
+    ms = {p: float(v[0]) for p, v in phases.items()}
+    inv = (ms.get("chunks", 0.0) + ms.get("prepare", 0.0) + ms.get("solve", 0.0)) * 1e-3
+    mul = (ms.get("score", 0.0) + ms.get("topk", 0.0)) * 1e-3
+    t = dict(inverse_hvp_s=inv, multiply_s=mul, total_s=inv + mul, wall_s=float(wall_s), n=int(n))
+    if log is not None:
+        log("Inverse HVP took %s sec" % inv)
+        log("Multiplying by %s train examples took %s sec" % (n, mul))
+        log("Total time is %s sec" % (inv + mul))
+    return t
+
+
 class GenericNeuralNet(object):
     MODEL_ID = None          # _lib.FIA_MODEL_MF / _lib.FIA_MODEL_NCF
     PARAM_NAMES = ()         # reference variable names, include/fia.h table order
@@ -238,10 +256,27 @@ class GenericNeuralNet(object):
                 "labels": np.asarray(data_set.labels, np.float32)[keep]}
 
     def retrain(self, num_steps, feed_dict):
-        """num_steps full-batch Adam steps on feed_dict's rows (gnn:344-347); one HIP graph
-        replay per step.  Only the trainer's parameters change (the FIA context keeps the
-        loaded model)."""
+        """GenericNeuralNet.retrain (gnn:344-347): num_steps Adam steps on ALL of feed_dict's
+        rows at once.  MF and NCF override it with the reference's mini-batch retrain
+        (mf:69-76, NCF.py:68-72); this full-batch form stays available to them as
+        retrain_full_batch."""
+        self.retrain_full_batch(num_steps, feed_dict)
+
+    def retrain_full_batch(self, num_steps, feed_dict):
+        """num_steps full-batch Adam steps on feed_dict's rows, one HIP graph replay per step
+        (opt-in fast path; not the MF / NCF reference procedure).  Only the trainer's
+        parameters change (the FIA context keeps the loaded model)."""
         self.trainer().full_batch(feed_dict["users"], feed_dict["items"], feed_dict["labels"], num_steps)
+
+    def _retrain_minibatch(self, num_steps, feed_dict):
+        """The MF / NCF retrain body: DataSet(feed rows) + num_steps steps on
+        next_batch(self.batch_size) (fill_feed_dict_with_batch, gnn:229-240)."""
+        x = np.stack([np.asarray(feed_dict["users"]), np.asarray(feed_dict["items"])], 1)
+        ds = DataSet(x, np.asarray(feed_dict["labels"]))
+        tr = self.trainer()
+        for _ in range(num_steps):
+            xb, yb = ds.next_batch(self.batch_size)
+            tr.step(xb[:, 0].astype(np.int64), xb[:, 1].astype(np.int64), yb)
 
     def reset_optimizer(self):
         """reset_optimizer_op (gnn:437-438)."""
@@ -356,7 +391,12 @@ class GenericNeuralNet(object):
             raise NotImplementedError("phantom points (train_idx=None) are not supported")
         if X is not None or Y is not None:
             raise ValueError("X and Y cannot be specified if train_idx is specified.")
-        if approx_type not in ("cg", "lissa"):
+        if approx_type == "lissa":
+            # gnn:503-508 dispatches 'lissa' to get_inverse_hvp_lissa (gnn:511-544); this
+            # build has one solver, the exact fp64 LDL^T, and does not pretend otherwise
+            raise NotImplementedError("approx_type='lissa' is not provided: the inverse HVP is the exact fp64 "
+                                      "solve (use approx_type='cg')")
+        if approx_type != "cg":
             raise ValueError("approx_type must be 'cg' or 'lissa'")
         if loss_type != "normal_loss":
             raise ValueError("Loss must be normal")
@@ -364,7 +404,16 @@ class GenericNeuralNet(object):
         t0 = time.time()
         self.test_index = test_indices[0]
         self.test_u, self.test_i = self._test_pair(self.test_index)
-        res = self.get_influence_batch(test_indices, K=0, full=True, return_x=True)
+        # the three RQ2 stage timers (mf:224-250) come from the library's HIP-event phases of
+        # this one call: inverse HVP = related lists + Hessian assembly + solve, multiplying =
+        # per-rating scoring (+ the fused top-K)
+        self.ctx.profile_read()
+        self.ctx.set_profiling(True)
+        try:
+            res = self.get_influence_batch(test_indices, K=0, full=True, return_x=True)
+        finally:
+            self.ctx.set_profiling(False)
+        phases = self.ctx.profile_read()
         self.train_indices_of_test_case = res["rel_idx"]
         x = res["x"][0]
         self.num_params = x.size
@@ -375,10 +424,8 @@ class GenericNeuralNet(object):
             fname = os.path.join(self.train_dir, "%s-%s-%s-test-%s.npz" % (
                 self.model_name, approx_type, loss_type, test_description))
             np.savez(fname, inverse_hvp=x)
-        dt = time.time() - t0
-        if self.verbose:
-            print("FIA test %s (u=%d, i=%d): %d related ratings, total time %.6f sec" % (
-                self.test_index, self.test_u, self.test_i, res["influence"].size, dt))
+        self.last_timing = rq2_timing(phases, res["influence"].size, time.time() - t0,
+                                      log=print if self.verbose else None)
         return res["influence"]
 
     def _split_theta(self, x):

@@ -40,6 +40,13 @@ class MF(GenericNeuralNet):
             self.PARAM_NAMES[4]: np.zeros(1, np.float32),
         }
 
+    def retrain(self, num_steps, feed_dict):
+        """MF.retrain (mf:69-76): reset_optimizer_op, then num_steps Adam steps on mini-batches
+        of self.batch_size drawn by DataSet.next_batch from the feed's rows (a fresh DataSet,
+        so the batches start at row 0 and shuffle at the epoch wrap, dataset.py:49-70)."""
+        self.reset_optimizer()
+        self._retrain_minibatch(num_steps, feed_dict)
+
     def _split_theta(self, x):
         k = self.embedding_size
         return [x[:k], x[k:2 * k], x[2 * k:2 * k + 1], x[2 * k + 1:2 * k + 2]]

@@ -159,7 +159,29 @@ def make_dataset(cfg, seed=0):
 
 def make_20m(seed=0, N=None, U=None, I=None):
     """ML-20M-shaped synthetic set: Zipf(1.0) item popularity, log-normal user
-    degrees, 2 held-out query pairs per user."""
+    degrees, 2 held-out query pairs per user.
+
+    Generation takes about a minute; with FIA_SYNTH_CACHE=<dir> the arrays are kept
+    there as an npz (written by this function, reloaded with allow_pickle=False), so
+    several runs inside one job share one draw."""
+    cache = os.environ.get("FIA_SYNTH_CACHE")
+    if cache:
+        path = os.path.join(cache, "synth20m_s%d_%s_%s_%s.npz" % (seed, N, U, I))
+        if os.path.exists(path):
+            with np.load(path, allow_pickle=False) as z:
+                return dict(train=(z["tu"], z["ti"], z["tr"]), test=(z["qu"], z["qi"], z["qr"]), valid=None,
+                            U=int(z["U"]), I=int(z["I"]))
+        d = _make_20m(seed, N, U, I)
+        os.makedirs(cache, exist_ok=True)
+        tmp = path + ".%d.tmp.npz" % os.getpid()
+        np.savez(tmp, tu=d["train"][0], ti=d["train"][1], tr=d["train"][2], qu=d["test"][0], qi=d["test"][1],
+                 qr=d["test"][2], U=d["U"], I=d["I"])
+        os.replace(tmp, path)
+        return d
+    return _make_20m(seed, N, U, I)
+
+
+def _make_20m(seed, N, U, I):
     cfg = dict(ML20M)
     U = U or cfg["U"]
     I = I or cfg["I"]

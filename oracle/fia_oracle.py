@@ -73,11 +73,15 @@ def mf_predict(params, k, users, items):
 
 def mf_query(params, k, train_users, train_items, train_ratings, u, i, wd, damping):
     """One MF FIA query. Returns dict(rel, n, v, H, x, influence) (fp64)."""
-    P, Q, bu, bi, g = _mf_tables(params, k)
     tu = np.asarray(train_users)
     ti = np.asarray(train_items)
-    x_f32 = np.stack([tu, ti], 1).astype(np.float32)
-    rel = related_indices(x_f32, u, i)
+    rel = related_indices(np.stack([tu, ti], 1).astype(np.float32), u, i)
+    return _mf_core(_mf_tables(params, k), k, tu, ti, train_ratings, u, i, wd, damping, rel)
+
+
+def _mf_core(tables, k, tu, ti, train_ratings, u, i, wd, damping, rel):
+    """mf_query's math for a given related list rel (mf:152-162, 237-246, 288-351)."""
+    P, Q, bu, bi, g = tables
     n = rel.size
     D = 2 * k + 2
     theta = np.concatenate([P[u], Q[i], [bu[u]], [bi[i]]])
@@ -154,12 +158,15 @@ def ncf_predict(params, k, users, items):
 
 def ncf_query(params, k, train_users, train_items, train_ratings, u, i, wd, damping):
     """One NCF FIA query. Returns dict(rel, n, v, H, x, influence) (fp64)."""
-    T = _ncf_tables(params, k)
-    h = k // 2
     tu = np.asarray(train_users)
     ti = np.asarray(train_items)
-    x_f32 = np.stack([tu, ti], 1).astype(np.float32)
-    rel = related_indices(x_f32, u, i)
+    rel = related_indices(np.stack([tu, ti], 1).astype(np.float32), u, i)
+    return _ncf_core(_ncf_tables(params, k), k, tu, ti, train_ratings, u, i, wd, damping, rel)
+
+
+def _ncf_core(T, k, tu, ti, train_ratings, u, i, wd, damping, rel):
+    """ncf_query's math for a given related list rel (ncf:181-191, 266-274, 317-380)."""
+    h = k // 2
     n = rel.size
     D = 4 * k
     theta = np.concatenate([T["Pm"][u], T["Qm"][i], T["Pg"][u], T["Qg"][i]])
@@ -198,3 +205,34 @@ def query(model, params, k, train_users, train_items, train_ratings, u, i, wd, d
 
 def num_params(model, k):
     return 2 * k + 2 if model == "MF" else 4 * k
+
+
+class CsrExact(object):
+    """The closed form above with the related lists read from a CSR (by user) / CSC (by
+    item) index of stably sorted train rows -- rel(u, i) is the same array as the O(N)
+    np.where scans give (mf:315-322) -- and the parameter tables converted once.  This is
+    the vectorized exact-solve CPU figure bench.py's cpu_baseline reports beside the
+    reference algorithm; it is a checker-side restatement, never
+    the product path."""
+
+    def __init__(self, model, params, k, train_users, train_items, train_ratings, wd, damping):
+        self.model, self.k, self.wd, self.damping = model, k, wd, damping
+        self.tu = np.asarray(train_users)
+        self.ti = np.asarray(train_items)
+        self.tr = np.asarray(train_ratings)
+        self.tables = _mf_tables(params, k) if model == "MF" else _ncf_tables(params, k)
+        self.lists = []
+        for ids in (self.tu, self.ti):
+            order = np.argsort(ids, kind="stable").astype(np.int64)
+            ptr = np.searchsorted(ids[order], np.arange(int(ids.max(initial=-1)) + 2), side="left")
+            self.lists.append((order, ptr))
+
+    def related(self, u, i):
+        (uo, up), (io, ip) = self.lists
+        ru = uo[up[u]:up[u + 1]] if u + 1 < up.size else uo[:0]
+        ri = io[ip[i]:ip[i + 1]] if i + 1 < ip.size else io[:0]
+        return np.concatenate([ru, ri])
+
+    def query(self, u, i):
+        core = _mf_core if self.model == "MF" else _ncf_core
+        return core(self.tables, self.k, self.tu, self.ti, self.tr, u, i, self.wd, self.damping, self.related(u, i))

@@ -25,8 +25,8 @@ def _model(kind, data, k=8, tmp="output", batch=500, lr=1e-2):
 
 @pytest.mark.parametrize("kind", ["MF", "NCF"])
 def test_graph_retrain_matches_eager(kind, tmp_path):
-    """retrain() replays one captured HIP graph per full-batch step; it must follow the
-    eager steps (embedding-gradient atomics reorder fp32 sums: tolerance, not bits)."""
+    """retrain_full_batch() replays one captured HIP graph per full-batch step; it must follow
+    the eager steps (embedding-gradient atomics reorder fp32 sums: tolerance, not bits)."""
     from rq1_small import small_data
     m = _model(kind, small_data(), tmp=tmp_path)
     tr = m.trainer()
@@ -37,7 +37,7 @@ def test_graph_retrain_matches_eager(kind, tmp_path):
     eager = tr.params_numpy()
     tr.set_params(p0)
     tr.opt.load_state(s0)
-    m.retrain(40, f)
+    m.retrain_full_batch(40, f)
     graph = tr.params_numpy()
     for n in m.PARAM_NAMES:
         assert np.allclose(graph[n], eager[n], rtol=1e-4, atol=1e-6), n

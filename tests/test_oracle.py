@@ -126,3 +126,22 @@ def test_ml1m_synthetic_fixture_is_reproducible():
         b, e = f["offsets"][q], f["offsets"][q + 1]
         assert np.array_equal(o["rel"], f["rel"][b:e])
         np.testing.assert_allclose(o["influence"], f["influence"][b:e], rtol=0, atol=1e-12 * np.abs(o["influence"]).max())
+
+
+@pytest.mark.parametrize("model", ["MF", "NCF"])
+def test_csr_exact_equals_scan_oracle(model):
+    """oracle.CsrExact (bench.py's vectorized exact-solve CPU figure) reads the related lists
+    from a stable CSR/CSC index: the same rel and bit-identical influence as the O(N)-scan
+    closed form, including the pair itself in train."""
+    rng = np.random.default_rng(4)
+    U, I, N = 60, 40, 900
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = synth.mf_params(U, I, 8, 1) if model == "MF" else synth.ncf_params(U, I, 8, 1)
+    c = fo.CsrExact(model, p, 8, tu, ti, tr, 1e-3, 1e-6)
+    for u, i in [(0, 0), (5, 7), (int(tu[3]), int(ti[3])), (U - 1, I - 1)]:
+        a = fo.query(model, p, 8, tu, ti, tr, u, i, 1e-3, 1e-6)
+        b = c.query(u, i)
+        assert np.array_equal(a["rel"], b["rel"])
+        assert np.array_equal(a["influence"], b["influence"])
