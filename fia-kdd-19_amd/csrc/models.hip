@@ -32,7 +32,8 @@ struct MFm {
   static constexpr int K = K_;
   static constexpr int Ds = K + 1;
   static constexpr int D = 2 * Ds;
-  static constexpr int SB = 2 * K + 3;          // per-side record: a, xs, bias, xsb, dup_other
+  static constexpr int SB = 2 * K + 4;          // per-side record: a, xs, bias, xsb, dup_other, pad
+                                                // (even: x_s starts 16-B aligned for k_score_mf_mfma)
   static constexpr int R = 4 + 2 * SB;          // header: inv_n, c_q, x.v, r-hat(u,i)
   static constexpr bool ncf = false;
   __device__ static bool decayed(int a) { return a < K; }
@@ -1715,6 +1716,239 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
 }
 
 // ------------------------------------------------------------------------------------
+// MF k in {32, 64}, K_top <= 1: entity-shared scoring on the f64 matrix cores.
+// A work item is <= 256 ratings of one entity's list x <= 15 batch queries sharing the
+// entity (the same work items as k_score_grouped_mf, query blocks of 15).  Per 16-rating
+// tile the scores of every (query, rating) pair are one 16x16 tile
+//   D = X . G^T      (v_mfma_f64_16x16x4_f64, K/4 slices of 4 coordinates)
+// with A rows = the block's queries' x (side block, k coordinates) and row 15 = the
+// entity's own embedding, so D[15][n] = theta_e . g_n gives the rating's residual
+// e_n = r-hat_n - y_n without a VALU dot product.  Slice s pairs coordinate (K/4) kk + s
+// of lane group kk = l >> 4: every lane loads K/4 CONTIGUOUS coordinates of its query's
+// x (once per work item) and of its rating's gathered row (per tile, 16-B loads).
+// MI355X runs f64 MFMA and f64 VALU on the same units (tools/mb_f64.hip: their times
+// add), so the epilogue keeps f64 work per pair to 3 ops:
+//   influence = fma(e * (2/n), D + x_bias, c_q / n)      (mf:240-246)
+// Top-1 candidates: per lane and query a running best over its tiles (|v| bits as an
+// integer key), reduced over the 16 lanes of a query row once per work item.  D layout
+// (f64 16x16x4): lane l register r = D[(l >> 4) + 4 r][l & 15]; A[m][k] from lane
+// m + 16 k, B[k][n] from lane n + 16 k.
+// ------------------------------------------------------------------------------------
+constexpr int kMfmaQB = 15;   // queries per work item (row 15 of A is the entity)
+
+// output stores of k_score_mf_mfma: 128-B runs of one query per 16 lanes, at the query's
+// arbitrary 8-B alignment; plain stores keep the straddled L2 lines until the next tile
+// completes them
+template <class T>
+__device__ __forceinline__ void st_out(T v, T* p) {
+#ifdef FIA_MFMA_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
+__device__ __forceinline__ long long topk_ikey(double v) {
+  // |v|'s bits order like |v| (non-negative doubles); NaN ranks below every number
+  const long long b = __double_as_longlong(v) & 0x7fffffffffffffffll;
+  return b > 0x7ff0000000000000ll ? -1ll : b;
+}
+
+template <class M, bool FULL>
+__global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
+    QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
+    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
+  constexpr int K = M::K, KS = K / 4, NF4 = KS / 4;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kk = lane >> 4, cn = lane & 15;     // k-group; A row / B column / D column
+  const int64_t n_items = wstart[nE];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  const double gbias = (double)A.t[4][0];
+  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
+    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int sd = g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(g - A.U) : g;
+    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int64_t gb = gstart[g] + (int64_t)qblk * kMfmaQB;
+    const int64_t gn = gstart[g + 1] - gb;
+    const int nq = gn < kMfmaQB ? (int)gn : kMfmaQB;
+    const int32_t* __restrict__ oth = A.other[sd] + lb;
+    const float* __restrict__ rat = A.rating[sd] + lb;
+    const int32_t* __restrict__ rw = A.row[sd] + lb;
+    const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];     // the other side's table
+    const float* __restrict__ bt = sd == 0 ? A.t[3] : A.t[2];
+    const float* __restrict__ Es = sd == 0 ? A.t[0] : A.t[1];    // this side's (the entity's) table
+    const double bself = (double)(sd == 0 ? A.t[2] : A.t[3])[e];
+    // A operand: lane (row cn, group kk) holds coordinates KS*kk .. KS*kk+KS-1 of its row
+    double a[KS];
+    if (cn == 15) {
+      const float4* src = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
+#pragma unroll
+      for (int f = 0; f < NF4; ++f) {
+        const float4 t = src[f];
+        a[4 * f] = t.x; a[4 * f + 1] = t.y; a[4 * f + 2] = t.z; a[4 * f + 3] = t.w;
+      }
+    } else {
+      const int32_t q = gq[gb + (cn < nq ? cn : nq - 1)];
+      const double2* src = reinterpret_cast<const double2*>(rec + (int64_t)q * M::R + 4 + sd * M::SB + K + KS * kk);
+#pragma unroll
+      for (int f = 0; f < KS / 2; ++f) {
+        const double2 t = src[f];
+        a[2 * f] = t.x; a[2 * f + 1] = t.y;
+      }
+    }
+    // per D row r (query m = kk + 4 r): influence = fma(e * al, D + xb, be) at outp[r][p]
+    double al[4], be[4], xb[4];
+    double* outp[4];
+    int64_t* relp[4];
+    int32_t dupo[4];
+    bool qv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = kk + 4 * r;
+      qv[r] = m < nq;
+      const int32_t q = gq[gb + (m < nq ? m : 0)];
+      const double* __restrict__ R = rec + (int64_t)q * M::R;
+      const double inv_n = R[0];
+      al[r] = 2.0 * inv_n;
+      be[r] = R[1] * inv_n;
+      xb[r] = R[4 + sd * M::SB + 2 * K + 1];
+      dupo[r] = qv[r] ? (int32_t)R[4 + sd * M::SB + 2 * K + 2] : -1;
+      const int64_t ob = qbase[4 * (int64_t)q + sd] + (int64_t)cidx * kChunk + cn;
+      outp[r] = influence + ob;
+      relp[r] = rel_idx + ob;
+    }
+    long long bk[4];
+    int bp[4];
+    double bv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { bk[r] = -2; bp[r] = 0x7fffffff; bv[r] = 0.0; }
+    const int ntl = (len + 15) / 16;
+    // software pipeline over the tiles, ring of three slots: the list entries of tile t + 2
+    // and the gathered rows of tile t + 1 are in flight while tile t is scored.  Positions
+    // past the chunk are clamped to its last entry (harmless loads, no branches).
+    int32_t so[3], sw[3];
+    float sy[3], sbo[3];
+    float4 sb[3][NF4];
+    auto load_list = [&](int t, int k3) {
+      const int p = 16 * t + cn < len ? 16 * t + cn : len - 1;
+      so[k3] = oth[p];
+      sy[k3] = rat[p];
+      sw[k3] = rw[p];
+    };
+    auto gather = [&](int k3) {
+      const float4* row = reinterpret_cast<const float4*>(T + (int64_t)so[k3] * K + KS * kk);
+#pragma unroll
+      for (int f = 0; f < NF4; ++f) sb[k3][f] = row[f];
+      sbo[k3] = bt[so[k3]];
+    };
+    auto tile = [&](int t, int k3) {
+      // the whole tile's B operands converted first: f64 VALU and f64 MFMA share the
+      // MI355X's double-precision units (tools/mb_f64.hip), so a conversion slotted between
+      // two MFMAs waits for the first to drain; the empty asm pins them before the chain
+      double bd[KS];
+#pragma unroll
+      for (int f = 0; f < NF4; ++f) {
+        bd[4 * f] = sb[k3][f].x; bd[4 * f + 1] = sb[k3][f].y; bd[4 * f + 2] = sb[k3][f].z; bd[4 * f + 3] = sb[k3][f].w;
+      }
+      if constexpr (KS == 16)
+        asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
+                     "+v"(bd[6]), "+v"(bd[7]), "+v"(bd[8]), "+v"(bd[9]), "+v"(bd[10]), "+v"(bd[11]),
+                     "+v"(bd[12]), "+v"(bd[13]), "+v"(bd[14]), "+v"(bd[15]));
+      else
+        asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
+                     "+v"(bd[6]), "+v"(bd[7]));
+      d4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int sl = 0; sl < KS; ++sl) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sl], bd[sl], acc, 0, 0, 0);
+      const int p = 16 * t + cn;                // position in the chunk of this lane's rating
+      const bool pv = p < len;
+      const int32_t o = so[k3], w = sw[k3];
+      const double y = (double)sy[k3];
+      // residual of rating cn: D[15][cn] lives in lane 48 + cn, register 3
+      const double dself = __shfl(acc[3], 48 + cn);
+      const double en = ((dself + bself) + (double)sbo[k3]) + gbias - y;
+      const bool dup = pv && (o == dupo[0] || o == dupo[1] || o == dupo[2] || o == dupo[3]);
+      if (__builtin_expect(__ballot(dup) != 0, 0)) {
+        // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (!(pv && qv[r] && o == dupo[r])) continue;
+          const int32_t q = gq[gb + kk + 4 * r];
+          const double* __restrict__ R = rec + (int64_t)q * M::R;
+          const double infl = fma((R[3] - y) * al[r], R[2], be[r]);
+          if (FULL || influence) st_out(infl, outp[r] + 16 * t);
+          if (FULL || rel_idx) st_out((int64_t)w, relp[r] + 16 * t);
+          const long long key = topk_ikey(infl);
+          if (key > bk[r]) { bk[r] = key; bp[r] = p; bv[r] = infl; }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = pv && qv[r] && o != dupo[r];
+        const double infl = fma(en * al[r], acc[r] + xb[r], be[r]);
+        if (ok) {
+          if (FULL || influence) st_out(infl, outp[r] + 16 * t);
+          if (FULL || rel_idx) st_out((int64_t)w, relp[r] + 16 * t);
+        }
+        const long long key = ok ? topk_ikey(infl) : -2ll;
+        const bool take = key > bk[r];
+        bk[r] = take ? key : bk[r];
+        bp[r] = take ? p : bp[r];
+        bv[r] = take ? infl : bv[r];
+      }
+    };
+    load_list(0, 0);
+    load_list(1, 1);
+    gather(0);
+    for (int t = 0; t < ntl; t += 3) {
+      load_list(t + 2, 2);
+      gather(1);
+      tile(t, 0);
+      if (t + 1 >= ntl) break;
+      load_list(t + 3, 0);
+      gather(2);
+      tile(t + 1, 1);
+      if (t + 2 >= ntl) break;
+      load_list(t + 4, 1);
+      gather(0);
+      tile(t + 2, 2);
+    }
+    if (K_top > 0) {
+      // best per query row: over the 16 lanes of the row (xor 1..8 stays inside the row)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        long long k1 = bk[r];
+        int p1 = bp[r];
+        double v1 = bv[r];
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          const long long k2 = __shfl_xor(k1, off);
+          const int p2 = __shfl_xor(p1, off);
+          const double v2 = __shfl_xor(v1, off);
+          if (k2 > k1 || (k2 == k1 && p2 < p1)) { k1 = k2; p1 = p2; v1 = v2; }
+        }
+        if (cn == 0 && qv[r]) {
+          const int32_t q = gq[gb + kk + 4 * r];
+          const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
+          const int64_t slot = (qb[2 + sd] + cidx) * K_top;
+          const int64_t poj = sd ? qb[1] - qb[0] : 0;    // |R_u| precedes item-side positions
+          const bool okk = k1 > -2;
+          cand_pos[slot] = okk ? (int32_t)(cidx * kChunk + p1 + poj) : -1;
+          cand_val[slot] = okk ? v1 : NAN;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // NCF entity-shared scoring.  Same work items, query blocks and outputs as
 // k_score_grouped_mf, but nothing of the MLP is recomputed here: per list position the
 // Gram pass stored g_mlp,j = W1_side . d1_j (coordinate-major, so every load below is a
@@ -2080,6 +2314,11 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // 429 k q/s; for MF k <= 16 the group build costs more than the shared gathers save
   // (ml-1m-ex 36.6 vs 39.3 M q/s).  NCF scoring is entity-shared only (k_score_ncf).
   const bool grouped = M::ncf || (c->score_mode >= 0 ? c->score_mode == 1 : M::K >= 32);
+  // MF k in {32, 64} at K <= 1: the f64-MFMA entity-shared kernel (query blocks of 15)
+  constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);
+  static const bool mfma_on = !getenv("FIA_NO_MFMA_SCORE");   // A/B knob: k_score_grouped_mf instead
+  const bool use_mfma = mfma_ok && grouped && K <= 1 && mfma_on;
+  const int qblock = use_mfma ? kMfmaQB : query_block<M>();
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
   const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
@@ -2097,7 +2336,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
-  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, query_block<M>(), s));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
@@ -2134,7 +2373,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
                          c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
                          c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-    else if constexpr (one_pass)
+    else if (use_mfma) {
+      if constexpr (mfma_ok) {
+        auto kern = (rel_idx && influence) ? k_score_mf_mfma<M, true> : k_score_mf_mfma<M, false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                           c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                           c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                           c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+      }
+    } else if constexpr (one_pass)
       hipLaunchKernelGGL(k_score_grouped_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
                          c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
                          c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
