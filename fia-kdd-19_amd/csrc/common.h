@@ -213,7 +213,7 @@ hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
 int64_t gram_chunk(int64_t want);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_items, int qb, hipStream_t s);
+                        int64_t max_items, int qb, hipStream_t s, int cpi = 1);
 
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported);

@@ -280,13 +280,14 @@ __global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __re
 
 // Single-pass decoupled look-back scan over the U + I entities (users, then items) of
 // the two per-entity counts of the entity-shared schedule: queries per entity (gcnt ->
-// gstart) and work items per entity, ceil(deg / kChunk) * ceil(gcnt / qb) (-> wstart).
+// gstart) and work items per entity, ceil(deg / (cpi kChunk)) * ceil(gcnt / qb) (->
+// wstart; a work item covers cpi consecutive list chunks).
 // Both exclusive prefixes (and the totals at [U + I]) in one launch: no library scan, no
 // count array.  tstate: two arrays of tile words (queries, work items); the last tile to
 // finish re-zeroes them and the two counters.
 __global__ __launch_bounds__(kScanThreads) void k_group_scan(
     const unsigned long long* __restrict__ gcnt, const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr,
-    int64_t U, int64_t I, int qb, int64_t* __restrict__ gstart, int64_t* __restrict__ wstart,
+    int64_t U, int64_t I, int qb, int cpi, int64_t* __restrict__ gstart, int64_t* __restrict__ wstart,
     unsigned long long* __restrict__ tstate, unsigned int* __restrict__ tctr) {
   __shared__ int s_tile;
   __shared__ int64_t s_wa[kScanThreads / 64], s_wb[kScanThreads / 64];
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kScanThreads) void k_group_scan(
     a = (int64_t)gcnt[t];
     if (a > 0) {
       const int64_t deg = t < U ? uptr[t + 1] - uptr[t] : iptr[t - U + 1] - iptr[t - U];
-      b = ((deg + kChunk - 1) / kChunk) * ((a + qb - 1) / qb);
+      b = ((deg + kChunk * cpi - 1) / (kChunk * cpi)) * ((a + qb - 1) / qb);
     }
   }
   int64_t ia = a, ib = b;
@@ -582,7 +583,7 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
 }
 
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_items, int qb, hipStream_t s) {
+                        int64_t max_items, int qb, hipStream_t s, int cpi) {
   const int64_t U = c->idx.U, I = c->idx.I, nE = U + I;
   const int64_t ntiles = (nE + 1 + kScanTile - 1) / kScanTile;
   FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
@@ -609,7 +610,7 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
   }
   unsigned int* ctr = reinterpret_cast<unsigned int*>(c->gscan.as<char>() + c->gscan.bytes - 16);
   hipLaunchKernelGGL(k_group_scan, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, c->gcnt.as<unsigned long long>(),
-                     uptr, iptr, U, I, qb, c->gstart.as<int64_t>(), c->wstart.as<int64_t>(),
+                     uptr, iptr, U, I, qb, cpi, c->gstart.as<int64_t>(), c->wstart.as<int64_t>(),
                      c->gscan.as<unsigned long long>(), ctr);
   FIA_HIP_TRY(hipGetLastError());
   if (Q > 0) {

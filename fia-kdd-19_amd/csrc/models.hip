@@ -1735,6 +1735,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
 // m + 16 k, B[k][n] from lane n + 16 k.
 // ------------------------------------------------------------------------------------
 constexpr int kMfmaQB = 15;   // queries per work item (row 15 of A is the entity)
+constexpr int kMfmaCPI = 4;   // list chunks (256 ratings) per work item: the item's setup loads amortised
 
 // output stores of k_score_mf_mfma: 128-B runs of one query per 16 lanes, at the query's
 // arbitrary 8-B alignment; plain stores keep the straddled L2 lines until the next tile
@@ -1761,7 +1762,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
-  constexpr int K = M::K, KS = K / 4, NF4 = KS / 4;
+  constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, CPI = kMfmaCPI, TPC = kChunk / 16;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kk = lane >> 4, cn = lane & 15;     // k-group; A row / B column / D column
@@ -1769,12 +1770,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
   const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
   const double gbias = (double)A.t[4][0];
   for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
-    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    // work item: CPI consecutive chunks (cg) of the entity's list x one query block
+    const int32_t g = witems[3 * wi], cg = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int64_t p0 = (int64_t)cg * (CPI * kChunk);   // first list position of the item
     const int sd = g >= A.U ? 1 : 0;
     const int32_t e = sd ? (int32_t)(g - A.U) : g;
-    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t lb = A.ptr[sd][e] + p0;
     const int64_t rem = A.ptr[sd][e + 1] - lb;
-    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int len = rem < CPI * kChunk ? (int)rem : CPI * kChunk;
     const int64_t gb = gstart[g] + (int64_t)qblk * kMfmaQB;
     const int64_t gn = gstart[g + 1] - gb;
     const int nq = gn < kMfmaQB ? (int)gn : kMfmaQB;
@@ -1807,7 +1810,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     double al[4], be[4], xb[4];
     double* outp[4];
     int64_t* relp[4];
-    int32_t dupo[4];
+    int32_t dupo[4], cpos[4];
+    int64_t cslot[4];
     bool qv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1820,7 +1824,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
       be[r] = R[1] * inv_n;
       xb[r] = R[4 + sd * M::SB + 2 * K + 1];
       dupo[r] = qv[r] ? (int32_t)R[4 + sd * M::SB + 2 * K + 2] : -1;
-      const int64_t ob = qbase[4 * (int64_t)q + sd] + (int64_t)cidx * kChunk + cn;
+      const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
+      const int64_t ob = qb[sd] + p0 + cn;
+      cslot[r] = qb[2 + sd] + (int64_t)cg * CPI;           // candidate slot of the item's first chunk
+      cpos[r] = (int32_t)(p0 + (sd ? qb[1] - qb[0] : 0));  // |R_u| precedes item-side positions
       outp[r] = influence + ob;
       relp[r] = rel_idx + ob;
     }
@@ -1847,6 +1854,31 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
 #pragma unroll
       for (int f = 0; f < NF4; ++f) sb[k3][f] = row[f];
       sbo[k3] = bt[so[k3]];
+    };
+    // per chunk (16 tiles): best of each query row over the row's 16 lanes (xor 1..8 stays
+    // inside the row) -> the chunk's candidate slot; then the running bests restart
+    auto emit = [&](int chunk) {
+      if (K_top <= 0) return;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        long long k1 = bk[r];
+        int p1 = bp[r];
+        double v1 = bv[r];
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          const long long k2 = __shfl_xor(k1, off);
+          const int p2 = __shfl_xor(p1, off);
+          const double v2 = __shfl_xor(v1, off);
+          if (k2 > k1 || (k2 == k1 && p2 < p1)) { k1 = k2; p1 = p2; v1 = v2; }
+        }
+        if (cn == 0 && qv[r]) {       // (no loads here: a load in the tile loop drains vmcnt)
+          const int64_t slot = (cslot[r] + chunk) * K_top;
+          const bool okk = k1 > -2;
+          cand_pos[slot] = okk ? (int32_t)(cpos[r] + p1) : -1;
+          cand_val[slot] = okk ? v1 : NAN;
+        }
+        bk[r] = -2; bp[r] = 0x7fffffff; bv[r] = 0.0;
+      }
     };
     auto tile = [&](int t, int k3) {
       // the whole tile's B operands converted first: f64 VALU and f64 MFMA share the
@@ -1903,6 +1935,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
         bp[r] = take ? p : bp[r];
         bv[r] = take ? infl : bv[r];
       }
+      if (t % TPC == TPC - 1 || t == ntl - 1) emit(t / TPC);
     };
     load_list(0, 0);
     load_list(1, 1);
@@ -1919,31 +1952,6 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
       load_list(t + 4, 1);
       gather(0);
       tile(t + 2, 2);
-    }
-    if (K_top > 0) {
-      // best per query row: over the 16 lanes of the row (xor 1..8 stays inside the row)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        long long k1 = bk[r];
-        int p1 = bp[r];
-        double v1 = bv[r];
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          const long long k2 = __shfl_xor(k1, off);
-          const int p2 = __shfl_xor(p1, off);
-          const double v2 = __shfl_xor(v1, off);
-          if (k2 > k1 || (k2 == k1 && p2 < p1)) { k1 = k2; p1 = p2; v1 = v2; }
-        }
-        if (cn == 0 && qv[r]) {
-          const int32_t q = gq[gb + kk + 4 * r];
-          const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
-          const int64_t slot = (qb[2 + sd] + cidx) * K_top;
-          const int64_t poj = sd ? qb[1] - qb[0] : 0;    // |R_u| precedes item-side positions
-          const bool okk = k1 > -2;
-          cand_pos[slot] = okk ? (int32_t)(cidx * kChunk + p1 + poj) : -1;
-          cand_val[slot] = okk ? v1 : NAN;
-        }
-      }
     }
   }
 }
@@ -2336,7 +2344,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
-  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
