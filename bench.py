@@ -79,6 +79,10 @@ def parse(argv=None):
                          "of the 8-GPU job)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
+    ap.add_argument("--spinup-seconds", type=float, default=None,
+                    help="untimed steps for at least this long before the warmup (default: 20 for the 20M configs, "
+                         "0 otherwise): a fresh MI355X runs the HBM-heavy scoring kernels ~15 %% slower for its "
+                         "first ~30 s of load")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rank-set", type=int, default=0,
@@ -444,6 +448,13 @@ def main():
                 a, b = a.cpu(), b.cpu()
             tg.start(a, b)
 
+    spinup = args.spinup_seconds if args.spinup_seconds is not None else (20.0 if cfg["data"] == "20m" else 0.0)
+    t_spin = time.time()
+    n_spin = 0
+    while time.time() - t_spin < spinup:
+        compute()
+        torch.cuda.synchronize(dev)
+        n_spin += 1
     for _ in range(args.warmup):
         compute()
         exchange()
@@ -533,6 +544,7 @@ def main():
                    "node_queries_per_step": node_queries, "n_train": int(tu.size),
                    "related_ratings_rank0_step": int(total), "topk": K, "query_batches": len(batches),
                    "query_order": args.query_order, "shard_of": shard_of, "hip_graph": use_graph,
+                   "spinup_steps": n_spin,
                    "dist_backend": backend if world > 1 else None,
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},
         "roofline": roofline,

@@ -1755,14 +1755,14 @@ __device__ __forceinline__ long long topk_ikey(double v) {
   return b > 0x7ff0000000000000ll ? -1ll : b;
 }
 
-template <class M, bool FULL>
+template <class M, bool FULL, int CPI, int SETUP>
 __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
-  constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, CPI = kMfmaCPI, TPC = kChunk / 16;
+  constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, TPC = kChunk / 16;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kk = lane >> 4, cn = lane & 15;     // k-group; A row / B column / D column
@@ -1790,7 +1790,26 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     const double bself = (double)(sd == 0 ? A.t[2] : A.t[3])[e];
     // A operand: lane (row cn, group kk) holds coordinates KS*kk .. KS*kk+KS-1 of its row
     double a[KS];
-    if (cn == 15) {
+    if constexpr (SETUP >= 2) {
+      // unconditional loads (clamped indices, selects after)
+      const int32_t qa = gq[gb + (cn < nq ? cn : nq - 1)];
+      const double2* srcx = reinterpret_cast<const double2*>(rec + (int64_t)qa * M::R + 4 + sd * M::SB + K + KS * kk);
+      const float4* srce = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
+      double2 xv[KS / 2];
+      float4 ev[NF4];
+#pragma unroll
+      for (int f = 0; f < KS / 2; ++f) xv[f] = srcx[f];
+#pragma unroll
+      for (int f = 0; f < NF4; ++f) ev[f] = srce[f];
+      const bool self_row = cn == 15;
+#pragma unroll
+      for (int f = 0; f < NF4; ++f) {
+        a[4 * f + 0] = self_row ? (double)ev[f].x : xv[2 * f].x;
+        a[4 * f + 1] = self_row ? (double)ev[f].y : xv[2 * f].y;
+        a[4 * f + 2] = self_row ? (double)ev[f].z : xv[2 * f + 1].x;
+        a[4 * f + 3] = self_row ? (double)ev[f].w : xv[2 * f + 1].y;
+      }
+    } else if (cn == 15) {
       const float4* src = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
 #pragma unroll
       for (int f = 0; f < NF4; ++f) {
@@ -1813,23 +1832,51 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     int32_t dupo[4], cpos[4];
     int64_t cslot[4];
     bool qv[4];
+    if constexpr (SETUP >= 1) {
+      // every query index first, then every per-query load (one wait)
+      int32_t qr[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = kk + 4 * r;
-      qv[r] = m < nq;
-      const int32_t q = gq[gb + (m < nq ? m : 0)];
-      const double* __restrict__ R = rec + (int64_t)q * M::R;
-      const double inv_n = R[0];
-      al[r] = 2.0 * inv_n;
-      be[r] = R[1] * inv_n;
-      xb[r] = R[4 + sd * M::SB + 2 * K + 1];
-      dupo[r] = qv[r] ? (int32_t)R[4 + sd * M::SB + 2 * K + 2] : -1;
-      const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
-      const int64_t ob = qb[sd] + p0 + cn;
-      cslot[r] = qb[2 + sd] + (int64_t)cg * CPI;           // candidate slot of the item's first chunk
-      cpos[r] = (int32_t)(p0 + (sd ? qb[1] - qb[0] : 0));  // |R_u| precedes item-side positions
-      outp[r] = influence + ob;
-      relp[r] = rel_idx + ob;
+      for (int r = 0; r < 4; ++r) {
+        const int m = kk + 4 * r;
+        qv[r] = m < nq;
+        qr[r] = gq[gb + (m < nq ? m : 0)];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double* __restrict__ R = rec + (int64_t)qr[r] * M::R;
+        const double inv_n = R[0];
+        al[r] = 2.0 * inv_n;
+        be[r] = R[1] * inv_n;
+        xb[r] = R[4 + sd * M::SB + 2 * K + 1];
+        const int32_t dup_other = (int32_t)R[4 + sd * M::SB + 2 * K + 2];
+        dupo[r] = qv[r] ? dup_other : -1;
+        const longlong2* __restrict__ qb = reinterpret_cast<const longlong2*>(qbase + 4 * (int64_t)qr[r]);
+        const longlong2 q01 = qb[0], q23 = qb[1];          // {out base user, item}, {slot base user, item}
+        const int64_t ob = (sd ? q01.y : q01.x) + p0 + cn;
+        cslot[r] = (sd ? q23.y : q23.x) + (int64_t)cg * CPI;
+        cpos[r] = (int32_t)(p0 + sd * (q01.y - q01.x));
+        outp[r] = influence + ob;
+        relp[r] = rel_idx + ob;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = kk + 4 * r;
+        qv[r] = m < nq;
+        const int32_t q = gq[gb + (m < nq ? m : 0)];
+        const double* __restrict__ R = rec + (int64_t)q * M::R;
+        const double inv_n = R[0];
+        al[r] = 2.0 * inv_n;
+        be[r] = R[1] * inv_n;
+        xb[r] = R[4 + sd * M::SB + 2 * K + 1];
+        dupo[r] = qv[r] ? (int32_t)R[4 + sd * M::SB + 2 * K + 2] : -1;
+        const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
+        const int64_t ob = qb[sd] + p0 + cn;
+        cslot[r] = qb[2 + sd] + (int64_t)cg * CPI;           // candidate slot of the item's first chunk
+        cpos[r] = (int32_t)(p0 + (sd ? qb[1] - qb[0] : 0));  // |R_u| precedes item-side positions
+        outp[r] = influence + ob;
+        relp[r] = rel_idx + ob;
+      }
     }
     long long bk[4];
     int bp[4];
@@ -2326,6 +2373,11 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);
   static const bool mfma_on = !getenv("FIA_NO_MFMA_SCORE");   // A/B knob: k_score_grouped_mf instead
   const bool use_mfma = mfma_ok && grouped && K <= 1 && mfma_on;
+  // A/B knobs of the MFMA kernel's variants (FIA_MFMA_CPI=1: one chunk per work item;
+  // FIA_MFMA_SETUP=1/2: batched / unconditional work-item setup loads)
+  static const int mfma_cpi = getenv("FIA_MFMA_CPI") ? atoi(getenv("FIA_MFMA_CPI")) : kMfmaCPI;
+  static const int mfma_setup = getenv("FIA_MFMA_SETUP") ? atoi(getenv("FIA_MFMA_SETUP")) : 1;
+  const int cpi_used = (mfma_cpi == 1 && rel_idx && influence) ? 1 : kMfmaCPI;
   const int qblock = use_mfma ? kMfmaQB : query_block<M>();
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
@@ -2344,7 +2396,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
-  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? cpi_used : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
@@ -2383,7 +2435,13 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
     else if (use_mfma) {
       if constexpr (mfma_ok) {
-        auto kern = (rel_idx && influence) ? k_score_mf_mfma<M, true> : k_score_mf_mfma<M, false>;
+        auto kern = k_score_mf_mfma<M, false, kMfmaCPI, 1>;
+        if (rel_idx && influence) {
+          kern = k_score_mf_mfma<M, true, kMfmaCPI, 0>;
+          if (mfma_cpi == 1) kern = mfma_setup == 2 ? k_score_mf_mfma<M, true, 1, 2> : mfma_setup == 1 ? k_score_mf_mfma<M, true, 1, 1> : k_score_mf_mfma<M, true, 1, 0>;
+          else if (mfma_setup == 1) kern = k_score_mf_mfma<M, true, kMfmaCPI, 1>;
+          else if (mfma_setup == 2) kern = k_score_mf_mfma<M, true, kMfmaCPI, 2>;
+        }
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
                            c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
                            c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
