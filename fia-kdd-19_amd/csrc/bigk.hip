@@ -25,6 +25,7 @@
 //     dotted with up to 8 query vectors.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -39,6 +40,9 @@ typedef double d4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ d4_t mfma4(double a, double b, d4_t c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+
+typedef __attribute__((address_space(3))) void* lds_vp;         // LDS-DMA destination
+typedef const __attribute__((address_space(1))) void* glb_vp;   // ... and its global source
 
 __device__ __forceinline__ double wsum(double x) {
 #pragma unroll
@@ -204,44 +208,53 @@ __global__ void k_l1_big(const float* __restrict__ emb, const float* __restrict_
   }
 }
 
-// NCF per train row (one wave per 16 user-major list positions), all products on the
-// f64 matrix cores (ncf:102-145, TF ReluGrad masks):
+// NCF per train row (one 4-wave workgroup per 16 list positions of side `pass`; the
+// waves split each product's output tiles), all products on the f64 matrix cores
+// (ncf:102-145, TF ReluGrad masks):
 //   z1 = L1u + L1i + b1,  z2 = relu(z1) W2 + b2,  d2 = 1[z2>0] W3m,
 //   d1 = 1[z1>0] (W2 d2),  r-hat = W3m.relu(z2) + W3g.(Pg_u*Qg_i) + b3
+// pass < 0 (full prepare): user-major positions, g_mlp of both sides for every row.
+// pass = sd (fia_prepare_for): side sd's positions, tiles without a cached entity's row
+// skipped, g_mlp of side sd only -- a cached entity's list is one contiguous run of its
+// side's positions, so the work is dense.  A row in both kinds of list gets its
+// residual from both passes: the same arithmetic, the same bits.
+constexpr int kRowWaves = 4;
 template <int K>
-__global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __restrict__ self0,
-                                                 const int32_t* __restrict__ other0, const int32_t* __restrict__ row0,
-                                                 const float* __restrict__ rat0, const double* __restrict__ l1u,
-                                                 const double* __restrict__ l1i, const float* __restrict__ b1,
-                                                 const float* __restrict__ W2, const float* __restrict__ b2,
-                                                 const float* __restrict__ W3, const float* __restrict__ b3,
-                                                 const float* __restrict__ Pg, const float* __restrict__ Qg,
-                                                 const float* __restrict__ W1, double* __restrict__ gm0,
-                                                 double* __restrict__ gm1, double* __restrict__ resid,
-                                                 const uint8_t* __restrict__ mark, int64_t U) {
-  constexpr int H = K / 2, LZ = K + 4, LD2 = H + 4;
+__global__ __launch_bounds__(64 * kRowWaves) void k_ncf_rows(
+    int64_t N, int pass, const int32_t* __restrict__ self0, const int32_t* __restrict__ other0,
+    const int32_t* __restrict__ row0, const float* __restrict__ rat0, const double* __restrict__ l1u,
+    const double* __restrict__ l1i, const float* __restrict__ b1, const float* __restrict__ W2,
+    const float* __restrict__ b2, const float* __restrict__ W3, const float* __restrict__ b3,
+    const float* __restrict__ Pg, const float* __restrict__ Qg, const float* __restrict__ W1,
+    double* __restrict__ gm0, double* __restrict__ gm1, double* __restrict__ resid,
+    const uint8_t* __restrict__ mark, int64_t U) {
+  constexpr int H = K / 2, LZ = K + 4, LD2 = H + 4, NW = kRowWaves;
   __shared__ double Z1[16 * LZ];
   __shared__ double D2[16 * LD2];
-  const int lane = threadIdx.x;
+  __shared__ double part_mlp[NW][16];
+  __shared__ double part_gmf[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ml = lane & 15, kl = lane >> 4;
   for (int64_t tile = blockIdx.x; tile * 16 < N; tile += gridDim.x) {
     const int64_t p0 = tile * 16;
     const int64_t my = p0 + ml;
     const bool v = my < N;
-    const int32_t u_l = v ? self0[my] : 0, i_l = v ? other0[my] : 0, j_l = v ? row0[my] : 0;
-    const float y_l = v ? rat0[my] : 0.f;
+    const int32_t s_l = v ? self0[my] : 0, o_l = v ? other0[my] : 0, j_l = v ? row0[my] : 0;
+    const int32_t u_l = pass == 1 ? o_l : s_l, i_l = pass == 1 ? s_l : o_l;
     // fia_prepare_for: g_mlp of a side is needed only for rows in a cached entity's list
-    const bool need_u = v && (!mark || mark[u_l]), need_i = v && (!mark || mark[U + i_l]);
+    const bool need_u = v && pass != 1 && (!mark || mark[u_l]);
+    const bool need_i = v && pass != 0 && (!mark || mark[U + i_l]);
     const bool any_u = __any(need_u), any_i = __any(need_i);
+    if (pass >= 0 && !(any_u || any_i)) continue;   // uniform over the workgroup (same tile)
     __syncthreads();
-    for (int r = 0; r < 16; ++r) {
+    for (int e = tid; e < 16 * K; e += 64 * NW) {
+      const int r = e / K, c = e % K;
       const int32_t u = __shfl(u_l, r), i = __shfl(i_l, r);
-      for (int c = lane; c < K; c += 64)
-        Z1[r * LZ + c] = l1u[(int64_t)u * K + c] + l1i[(int64_t)i * K + c] + (double)b1[c];
+      Z1[r * LZ + c] = l1u[(int64_t)u * K + c] + l1i[(int64_t)i * K + c] + (double)b1[c];
     }
     __syncthreads();
     double mlp[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int t = 0; t < H / 16; ++t) {
+    for (int t = w; t < H / 16; t += NW) {
       d4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
       for (int kk = 0; kk < K; kk += 4) {
@@ -258,8 +271,27 @@ __global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __res
         D2[(kl + 4 * r) * LD2 + d] = on ? w3m : 0.0;
       }
     }
+    // this wave's MLP partial of row kl + 4r sits in lane 16 kl after the reduction
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double m = mlp[r];
+      m += __shfl_xor(m, 1);
+      m += __shfl_xor(m, 2);
+      m += __shfl_xor(m, 4);
+      m += __shfl_xor(m, 8);
+      if (ml == 0) part_mlp[w][kl + 4 * r] = m;
+    }
+    // gmf dot of rows w, w + NW, ... (wave-wide over the k coordinates)
+    for (int r = w; r < 16; r += NW) {
+      const int32_t u = __shfl(u_l, r), i = __shfl(i_l, r);
+      double part = 0.0;
+      for (int c = lane; c < K; c += 64)
+        part = fma((double)W3[H + c] * (double)Pg[(int64_t)u * K + c], (double)Qg[(int64_t)i * K + c], part);
+      part = wsum(part);
+      if (lane == 0) part_gmf[r] = part;
+    }
     __syncthreads();
-    for (int t = 0; t < K / 16; ++t) {
+    for (int t = w; t < K / 16; t += NW) {
       d4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
       for (int kk = 0; kk < H; kk += 4)
@@ -277,7 +309,7 @@ __global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __res
     for (int sd = 0; sd < 2; ++sd) {
       if (!(sd ? any_i : any_u)) continue;
       double* __restrict__ gm = sd ? gm1 : gm0;
-      for (int t = 0; t < K / 16; ++t) {
+      for (int t = w; t < K / 16; t += NW) {
         d4_t acc = {0.0, 0.0, 0.0, 0.0};
         const float* __restrict__ wrow = W1 + (int64_t)(sd * K + 16 * t + ml) * K;
 #pragma unroll 4
@@ -290,30 +322,12 @@ __global__ __launch_bounds__(64) void k_ncf_rows(int64_t N, const int32_t* __res
         }
       }
     }
-    // r-hat per row: the MLP part sits in the 16 lanes of group (row & 3), register row >> 2
+    if (w == 0 && lane < 16 && v) {
+      double m = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      double m = mlp[r];
-      m += __shfl_xor(m, 1);
-      m += __shfl_xor(m, 2);
-      m += __shfl_xor(m, 4);
-      m += __shfl_xor(m, 8);
-      mlp[r] = m;
+      for (int q = 0; q < NW; ++q) m += part_mlp[q][lane];
+      resid[j_l] = m + part_gmf[lane] + (double)b3[0] - (double)rat0[my];
     }
-    double t0 = __shfl(mlp[0], (ml & 3) * 16), t1 = __shfl(mlp[1], (ml & 3) * 16);
-    double t2 = __shfl(mlp[2], (ml & 3) * 16), t3 = __shfl(mlp[3], (ml & 3) * 16);
-    const int rsel = ml >> 2;
-    const double my_mlp = rsel == 0 ? t0 : rsel == 1 ? t1 : rsel == 2 ? t2 : t3;
-    double my_gmf = 0.0;
-    for (int r = 0; r < 16; ++r) {
-      const int32_t u = __shfl(u_l, r), i = __shfl(i_l, r);
-      double part = 0.0;
-      for (int c = lane; c < K; c += 64)
-        part = fma((double)W3[H + c] * (double)Pg[(int64_t)u * K + c], (double)Qg[(int64_t)i * K + c], part);
-      part = wsum(part);
-      if (ml == r) my_gmf = part;
-    }
-    if (lane < 16 && v) resid[j_l] = my_mlp + my_gmf + (double)b3[0] - (double)y_l;
   }
 }
 
@@ -830,6 +844,399 @@ __global__ __launch_bounds__(solve_threads<NP>()) void k_big_solve(BigArgs A, co
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Batched blocked LDL^T of the side systems (CPL = false, NP % 64 == 0).  The systems of
+// a chunk are factored together, one launch pair per 64-column panel, so thousands of
+// independent workgroups keep every CU's memory pipeline busy -- the persistent
+// one-workgroup-per-system kernel above spends most of its time waiting on its own
+// panel chain.  Per system slab: L (column-major, LDR = NP + 16 rows, row NP the
+// right-hand side v^T), d (NP) and W = (D11 L11^T)^-1 of the current panel (64 x 64).
+//   k_bs_dupd : the panel's diagonal block A - L D L^T (MFMA, k-steps split over four
+//               waves);
+//   k_bs_dfac : its LDL^T in one wave (readlane broadcasts), W by forward substitution
+//               (lane j: column j of L11^-1);
+//   k_bs_trail: per 16-row tile below the block, the panel update (MFMA, L streamed)
+//               and the triangular solve as one more MFMA product, P W, stored as L;
+//   k_bs_back : L^T x = y (y = row NP of L) and the scoring record.
+// ------------------------------------------------------------------------------------
+constexpr int kBsNB = 64;                          // panel width
+constexpr int kBsMG = 2;                           // row tiles per k_bs_trail wave
+constexpr int64_t kBsScratch = (int64_t)8 << 30;   // bytes of factor slabs per chunk
+
+template <int NP>
+__host__ __device__ constexpr int64_t bs_slab() { return (int64_t)(NP + 16) * NP + NP + kBsNB * kBsNB; }
+
+// wave-local LDS hand-off: a wave's LDS operations complete in order; this only keeps
+// the compiler from moving them across the exchange
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one side system (mf:164-251 / ncf:193-280 restricted to one side): rows/cols [0, Ds)
+// (2/n) A_e + wd M + damping I, identity padding to NP, row NP the right-hand side v
+template <class M, int NP>
+struct SideSys {
+  const double* G;
+  const double* vv;
+  double s2n, wd, damping;
+  // branch-free (every lane loads from a valid address, then selects), so the loads of
+  // a tile's elements issue back to back instead of one exec-masked round trip each
+  __device__ double at(int r, int c) const {
+    const bool in = r < M::Ds && c < M::Ds;
+    const int rr = in ? r : 0, cc = in ? c : 0;
+    const int hi = rr > cc ? rr : cc, lo = rr > cc ? cc : rr;
+    const double g = G[tile_off(M::T, hi >> 4, lo >> 4) * 256 + (hi & 15) + 16 * (lo & 15)];
+    const double v = vv[c < NP ? c : NP - 1];
+    const double h = s2n * g + (r == c ? (M::decayed(r) ? wd : 0.0) + damping : 0.0);
+    // 0/1 weights rather than selects of the loaded values (a select lets the compiler
+    // sink each load into its own exec-masked branch and wait on it there)
+    const double fv = (r == NP && c < NP) ? 1.0 : 0.0, fh = (r < NP && in) ? 1.0 : 0.0;
+    const double fp = (r < NP && !in && r == c) ? 1.0 : 0.0;
+    return fma(fv, v, fma(fh, h, fp));
+  }
+};
+
+template <class M, int NP>
+__device__ __forceinline__ SideSys<M, NP> side_sys(const BigArgs& A, int code, const double* __restrict__ qwork) {
+  constexpr int64_t GW = gram_words<M>();
+  const int64_t q = code >> 1;
+  const int sd = code & 1;
+  const double* __restrict__ qw = qwork + q * M::QW;
+  SideSys<M, NP> S;
+  S.s2n = 2.0 / qw[0];
+  S.vv = qw + 8 + sd * M::NPs;
+  if (sd == 0) {
+    const int32_t u = A.qu[q];
+    S.G = A.gram[0] + (int64_t)(A.slot[0] ? A.slot[0][u] : u) * GW;
+  } else {
+    const int32_t i = A.qi[q];
+    S.G = A.gram[1] + (int64_t)(A.slot[1] ? A.slot[1][i] : i) * GW;
+  }
+  S.wd = A.wd;
+  S.damping = A.damping;
+  return S;
+}
+
+// diagonal block of panel c0: A - L[c0:c0+64, :c0] D L[c0:c0+64, :c0]^T (lower tiles
+// (rt, ct <= rt); wave w takes k-steps w, w + 4, ... through a register ring), stored
+// into the slab's W area for k_bs_dfac
+template <class M, int NP>
+__global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __restrict__ list, int w0, int c0,
+                                                 const double* __restrict__ qwork, double* __restrict__ lscr) {
+  constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, PD = 4;
+  __shared__ double T[NB * LT];
+  const int w = w0 + (int)blockIdx.x;
+  if (w >= list[0]) return;
+  const SideSys<M, NP> H = side_sys<M, NP>(A, list[1 + w], qwork);
+  double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * bs_slab<NP>();
+  const double* __restrict__ dd = Ls + (int64_t)LDR * NP;
+  double* __restrict__ Dg = Ls + (int64_t)LDR * NP + NP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < NB * NB / 256; ++i) {
+    const int e = tid + 256 * i, r = e >> 6, cc = e & 63;
+    T[r * LT + cc] = cc <= r ? H.at(c0 + r, c0 + cc) : 0.0;
+  }
+  d4_t acc[10];
+#pragma unroll
+  for (int t = 0; t < 10; ++t) acc[t] = d4_t{0.0, 0.0, 0.0, 0.0};
+  const int nst = c0 >> 2;
+  const int nmy = nst > wave ? (nst - wave + 3) >> 2 : 0;
+  double ra[PD][4], rd[PD];
+  auto ld = [&](int m, double (&a)[4], double& d) {
+    const int k = 4 * (wave + 4 * m) + kl;
+    const double* __restrict__ Lc = Ls + (int64_t)k * LDR + c0;
+    d = dd[k];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) a[rt] = Lc[16 * rt + ml];
+  };
+#pragma unroll
+  for (int d = 0; d < PD; ++d)
+    if (d < nmy) ld(d, ra[d], rd[d]);
+  for (int m0 = 0; m0 < nmy; m0 += PD) {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      if (m0 + d < nmy) {
+        int t = 0;
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          const double a = -ra[d][rt] * rd[d];
+#pragma unroll
+          for (int ct = 0; ct <= rt; ++ct, ++t) acc[t] = mfma4(a, ra[d][ct], acc[t]);
+        }
+        if (m0 + d + PD < nmy) ld(m0 + d + PD, ra[d], rd[d]);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+      int t = 0;
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int ct = 0; ct <= rt; ++ct, ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) T[(16 * rt + kl + 4 * r) * LT + 16 * ct + ml] += acc[t][r];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < NB * NB; e += 256) Dg[e] = T[(e & 63) * LT + (e >> 6)];   // column-major
+}
+
+// LDL^T of the updated diagonal block (one wave per system; lane r owns row r, readlane
+// broadcasts, no LDS), L11 and d into the slab, then W = L11^-T D^-1 (lane j: column j
+// of L11^-1 by forward substitution), stored transposed and XOR-swizzled,
+// Wt[n][j ^ 4 (n & 7)] = W[j][n], so k_bs_trail's B-operand reads from its linear LDS copy
+// are two-way at most
+template <class M, int NP>
+__global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list, int w0, int c0,
+                                                double* __restrict__ lscr) {
+  constexpr int LDR = NP + 16, NB = kBsNB;
+  const int w = w0 + (int)blockIdx.x;
+  if (w >= list[0]) return;
+  double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * bs_slab<NP>();
+  double* __restrict__ dd = Ls + (int64_t)LDR * NP;
+  double* __restrict__ W = dd + NP;
+  const int lane = threadIdx.x;
+  // entries right of a lane's diagonal become garbage and are never read
+  double a[NB];
+#pragma unroll
+  for (int t = 0; t < NB; ++t) a[t] = W[t * NB + lane];      // block stored column-major
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const double dj = readlane_dbl(a[j], j);
+    const double f = lane > j ? a[j] / dj : 0.0;
+#pragma unroll
+    for (int t = j + 1; t < NB; ++t) a[t] = fma(-f, readlane_dbl(a[j], t), a[t]);
+  }
+  double dl = a[0];
+#pragma unroll
+  for (int t = 1; t < NB; ++t) dl = t == lane ? a[t] : dl;
+  dd[c0 + lane] = dl;
+  const double rdl = 1.0 / dl;
+#pragma unroll
+  for (int t = 0; t < NB; ++t) {                            // a[t] becomes L11[lane][t], t < lane
+    a[t] = t < lane ? a[t] * readlane_dbl(rdl, t) : 0.0;
+    if (t < lane) Ls[(int64_t)(c0 + t) * LDR + c0 + lane] = a[t];
+  }
+  // lane j: column j of L11^-1 (x_m = 0 for m < j)
+  double x[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    double s = i == lane ? 1.0 : 0.0;
+#pragma unroll
+    for (int m = 0; m < i; ++m) s = fma(-readlane_dbl(a[m], i), x[m], s);
+    x[i] = s;
+  }
+#pragma unroll
+  for (int n = 0; n < NB; ++n) W[n * NB + (lane ^ (4 * (n & 7)))] = x[n] * readlane_dbl(rdl, n);
+}
+
+template <class M, int NP>
+__global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __restrict__ list, int w0, int c0,
+                                                  int tpb, const double* __restrict__ qwork,
+                                                  double* __restrict__ lscr) {
+  constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, MG = kBsMG, PDT = 5;
+  __shared__ double Pw[4][16 * LT];
+  __shared__ double Ws[NB * NB];
+  const int sys = (int)blockIdx.x / tpb, grp = (int)blockIdx.x - sys * tpb;
+  const int w = w0 + sys;
+  if (w >= list[0]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
+  double* __restrict__ Ls = lscr + (int64_t)sys * bs_slab<NP>();
+  const double* __restrict__ dd = Ls + (int64_t)LDR * NP;
+  const double* __restrict__ W = dd + NP;
+  // W of this panel (k_bs_dfac) into LDS by DMA, landing while the panel update runs
+#pragma unroll
+  for (int i = 0; i < NB * NB / 512; ++i)
+    __builtin_amdgcn_global_load_lds((glb_vp)(W + 2 * (i * 256 + tid)), (lds_vp)(Ws + 2 * (i * 256 + wave * 64)), 16,
+                                     0, 0);
+  const int R0 = c0 + NB + 16 * MG * (4 * grp + wave);     // first row of this wave's tiles
+  const bool active = R0 < LDR;
+  const int ng = (LDR - R0) / 16 < MG ? (LDR - R0) / 16 : MG;
+  const SideSys<M, NP> H = side_sys<M, NP>(A, list[1 + w], qwork);
+  d4_t acc[MG][4];
+#pragma unroll
+  for (int m = 0; m < MG; ++m)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[m][ct][r] = H.at(R0 + 16 * m + kl + 4 * r, c0 + 16 * ct + ml);
+  // panel update: k-steps (4 factored columns each) through a ring of PDT register slots
+  const int nst = active ? c0 >> 2 : 0;
+  double ra[PDT][MG], rb[PDT][4], rd[PDT];
+  auto ld = [&](int st, double (&a)[MG], double (&b)[4], double& d) {
+    const int k = 4 * st + kl;
+    const double* __restrict__ Lc = Ls + (int64_t)k * LDR;
+    d = dd[k];
+#pragma unroll
+    for (int m = 0; m < MG; ++m) a[m] = Lc[R0 + 16 * m + ml];     // rows past LDR: never used (m >= ng)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) b[ct] = Lc[c0 + 16 * ct + ml];
+  };
+#pragma unroll
+  for (int d = 0; d < PDT; ++d)
+    if (d < nst) ld(d, ra[d], rb[d], rd[d]);
+  for (int s0 = 0; s0 < nst; s0 += PDT) {
+#pragma unroll
+    for (int d = 0; d < PDT; ++d) {
+      if (s0 + d < nst) {
+#pragma unroll
+        for (int m = 0; m < MG; ++m) {
+          const double a = -ra[d][m] * rd[d];
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[m][ct] = mfma4(a, rb[d][ct], acc[m][ct]);
+        }
+        if (s0 + d + PDT < nst) ld(s0 + d + PDT, ra[d], rb[d], rd[d]);
+      }
+    }
+  }
+  __syncthreads();   // W landed
+  if (!active) return;
+  // triangular solve: L[rows][panel] = P W (W upper triangular), through this wave's LDS tile
+  double* __restrict__ P = Pw[wave];
+#pragma unroll
+  for (int m = 0; m < MG; ++m) {
+    if (m >= ng) continue;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = acc[m][ct][r];
+    wave_lds_sync();
+    double pa[NB / 4];
+#pragma unroll
+    for (int s = 0; s < NB / 4; ++s) pa[s] = P[ml * LT + 4 * s + kl];
+    d4_t o[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      o[ct] = d4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4 * ct + 4; ++s) o[ct] = mfma4(pa[s], Ws[(16 * ct + ml) * NB + ((4 * s + kl) ^ (4 * (ml & 7)))], o[ct]);
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = o[ct][r];
+    wave_lds_sync();
+    const int Rm = R0 + 16 * m;
+#pragma unroll
+    for (int i = 0; i < NB / 4; ++i) Ls[(int64_t)(c0 + kl + 4 * i) * LDR + Rm + ml] = P[ml * LT + kl + 4 * i];
+    wave_lds_sync();
+  }
+}
+
+template <class M, int NP>
+__global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __restrict__ list, int w0,
+                                                 const double* __restrict__ qwork, double* __restrict__ lscr,
+                                                 double* __restrict__ xb, double* __restrict__ rec) {
+  constexpr int K = M::K, NPs = M::NPs, Ds = M::Ds, LDR = NP + 16, kST = 512, kSW = kST / 64;
+  constexpr int CPT = (NP + kST - 1) / kST, BW = CPT == 1 ? 32 : 16;
+  __shared__ double xs[NP];
+  __shared__ double W11[BW * BW];
+  __shared__ double red[64];
+  const int w = w0 + (int)blockIdx.x;
+  if (w >= list[0]) return;
+  const int code = list[1 + w];
+  const int64_t q = code >> 1;
+  const int sd = code & 1;
+  const double* __restrict__ qw = qwork + q * M::QW;
+  const double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * bs_slab<NP>();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // L^T x = y, y_c = L[NP][c]; BW-column blocks from the end: a one-wave triangle per
+  // block (staged in W11), then the GEMV update of the earlier entries.  The next
+  // block's operands (the triangle and the GEMV columns) are loaded behind the current one.
+  constexpr int WPT = BW * BW / kST > 0 ? BW * BW / kST : 1;   // triangle entries per thread
+  auto fetch = [&](int b0, double (&lv)[CPT][BW], double (&wl)[WPT]) {
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) {
+      const int c = tid + cc * kST;
+#pragma unroll
+      for (int t = 0; t < BW; ++t) lv[cc][t] = c < b0 ? Ls[(int64_t)c * LDR + b0 + t] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) {          // W11[c][t] = L[b0 + t][b0 + c], t > c
+      const int e = tid + k * kST, cc = e / BW, t = e - cc * BW;
+      wl[k] = (e < BW * BW && t > cc) ? Ls[(int64_t)(b0 + cc) * LDR + b0 + t] : 0.0;
+    }
+  };
+  auto process = [&](int b0, const double (&lv)[CPT][BW], const double (&wl)[WPT]) {
+#pragma unroll
+    for (int k = 0; k < WPT; ++k)
+      if (tid + k * kST < BW * BW) W11[tid + k * kST] = wl[k];
+    __syncthreads();
+    if (wave == 0) {
+      double val = lane < BW ? xs[b0 + lane] : 0.0;
+      const double* __restrict__ Wc = W11 + (lane < BW ? lane : 0) * BW;
+#pragma unroll
+      for (int t = BW - 1; t >= 0; --t) {
+        const double xt = readlane_dbl(val, t);
+        if (lane < t) val = fma(-Wc[t], xt, val);
+      }
+      if (lane < BW) xs[b0 + lane] = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) {
+      const int c = tid + cc * kST;
+      if (c < b0) {
+        double s = xs[c];
+#pragma unroll
+        for (int t = 0; t < BW; ++t) s = fma(-lv[cc][t], xs[b0 + t], s);
+        xs[c] = s;
+      }
+    }
+    __syncthreads();
+  };
+  for (int c = tid; c < NP; c += kST) xs[c] = Ls[(int64_t)c * LDR + NP];
+  double lvA[CPT][BW], lvB[CPT][BW], wlA[WPT], wlB[WPT];
+  const int blast = ((NP - 1) / BW) * BW;
+  fetch(blast, lvA, wlA);
+  for (int b0 = blast; b0 >= 0; b0 -= 2 * BW) {
+    if (b0 - BW >= 0) fetch(b0 - BW, lvB, wlB);
+    process(b0, lvA, wlA);
+    if (b0 - BW < 0) break;
+    if (b0 - 2 * BW >= 0) fetch(b0 - 2 * BW, lvA, wlA);
+    process(b0 - BW, lvB, wlB);
+  }
+  // padded solution, this side's partial sums and scoring record (as k_big_solve)
+  const int32_t u = A.qu[q], i = A.qi[q];
+  const double* __restrict__ vsd = qw + 8 + sd * NPs;
+  const double* __restrict__ th = qw + 8 + 2 * NPs + sd * NPs;
+  double* __restrict__ xo = xb + q * 2 * NPs + sd * NPs;
+  double cq = 0.0, xv = 0.0;
+  for (int a = tid; a < NPs; a += kST) {
+    const double xa = xs[a];
+    xo[a] = xa;
+    if (a < Ds) {
+      if (M::decayed(a)) cq = fma(xa, th[a], cq);
+      xv = fma(xa, vsd[a], xv);
+    }
+  }
+  cq = bsum<kSW>(cq, red);
+  xv = bsum<kSW>(xv, red);
+  double* __restrict__ R = rec + q * M::R;
+  double* __restrict__ S = R + 8 + sd * M::SB;
+  if (tid == 0) {
+    R[4 + 2 * sd] = A.wd * cq;
+    R[5 + 2 * sd] = xv;
+  }
+  if constexpr (!M::ncf) {
+    for (int a = tid; a <= K; a += kST) S[a] = xs[a];
+    if (tid == 0) S[K + 1] = (double)(sd ? u : i);
+  } else {
+    for (int c = tid; c < K; c += kST) {
+      S[c] = xs[c];
+      S[K + c] = (double)A.t[8][M::H + c] * xs[K + c];
+    }
+    if (tid == 0) S[2 * K] = (double)(sd ? u : i);
+  }
+}
+
 // per-query record header and x in the reference theta order
 template <class M>
 __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __restrict__ qwork,
@@ -1141,10 +1548,11 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
       FIA_HIP_TRY(hipGetLastError());
       FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1), s));
     }
-    if (N > 0) {
-      hipLaunchKernelGGL(k_ncf_rows<K>, dim3(grid_cap((N + 15) / 16, 65536)), dim3(64), 0, s, N,
-                         c->self[0].as<int32_t>(), X.side[0].other.as<int32_t>(), X.side[0].row.as<int32_t>(),
-                         X.side[0].rating.as<float>(), c->l1[0].as<double>(), c->l1[1].as<double>(), c->p.t[5],
+    for (int pass = qu ? 0 : -1; N > 0 && pass < (qu ? 2 : 0); ++pass) {
+      const int sd = pass < 0 ? 0 : pass;
+      hipLaunchKernelGGL(k_ncf_rows<K>, dim3(grid_cap((N + 15) / 16, 65536)), dim3(64 * kRowWaves), 0, s, N, pass,
+                         c->self[sd].as<int32_t>(), X.side[sd].other.as<int32_t>(), X.side[sd].row.as<int32_t>(),
+                         X.side[sd].rating.as<float>(), c->l1[0].as<double>(), c->l1[1].as<double>(), c->p.t[5],
                          c->p.t[6], c->p.t[7], c->p.t[8], c->p.t[9], c->p.t[2], c->p.t[3], c->p.t[4],
                          c->gm[0].as<double>(), c->gm[1].as<double>(), c->resid.as<double>(),
                          qu ? c->mark.as<uint8_t>() : (const uint8_t*)nullptr, n_ent[0]);
@@ -1185,6 +1593,39 @@ hipError_t launch_solve(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int
   return hipGetLastError();
 }
 
+// side systems through the batched panel kernels, chunks of <= kBsScratch bytes of slabs;
+// list[0] (the device-side count) bounds every launch, max_sys only sizes them
+template <class M, int NP>
+hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int32_t* list, hipStream_t s) {
+  static_assert(NP % kBsNB == 0, "batched solve needs whole panels");
+  if (max_sys <= 0) return hipSuccess;
+  constexpr int64_t slab = bs_slab<NP>();
+  static const int64_t scratch = getenv("FIA_BS_SCRATCH_MB") ? atoll(getenv("FIA_BS_SCRATCH_MB")) << 20 : kBsScratch;
+  int64_t S = scratch / (int64_t)(sizeof(double) * slab);
+  S = S < 1 ? 1 : (S > max_sys ? max_sys : S);
+  FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(S * slab), s));
+  for (int64_t w0 = 0; w0 < max_sys; w0 += S) {
+    const int64_t n = max_sys - w0 < S ? max_sys - w0 : S;
+    for (int c0 = 0; c0 < NP; c0 += kBsNB) {
+      hipLaunchKernelGGL((k_bs_dupd<M, NP>), dim3((unsigned)n), dim3(256), 0, s, A, list, (int)w0, c0,
+                         c->qwork.as<double>(), c->lscr.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL((k_bs_dfac<M, NP>), dim3((unsigned)n), dim3(64), 0, s, list, (int)w0, c0,
+                         c->lscr.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+      const int tiles = (NP + 16 - c0 - kBsNB) / 16;
+      const int tpb = (tiles + 4 * kBsMG - 1) / (4 * kBsMG);
+      hipLaunchKernelGGL((k_bs_trail<M, NP>), dim3((unsigned)(n * tpb)), dim3(256), 0, s, A, list, (int)w0, c0, tpb,
+                         c->qwork.as<double>(), c->lscr.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL((k_bs_back<M, NP>), dim3((unsigned)n), dim3(512), 0, s, A, list, (int)w0,
+                       c->qwork.as<double>(), c->lscr.as<double>(), c->xb.as<double>(), c->rec.as<double>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
 template <class M>
 hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                           int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
@@ -1210,7 +1651,14 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   hipLaunchKernelGGL(k_big_prologue<M>, dim3(grid_cap(Q, 1 << 20)), dim3(256), 0, s, A, Q, c->qwork.as<double>(),
                      c->syslist.as<int32_t>(), c->cpllist.as<int32_t>());
   FIA_HIP_TRY(hipGetLastError());
-  FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+  if constexpr (NPs % kBsNB == 0) {
+    if (!getenv("FIA_BIG_SOLVE_PERSISTENT"))
+      FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+    else
+      FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+  } else {
+    FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+  }
   FIA_HIP_TRY((launch_solve<M, 2 * NPs, true>(c, A, Q, c->cpllist.as<int32_t>(), s)));
   hipLaunchKernelGGL(k_big_finish<M>, dim3(grid_cap(Q, 1 << 20)), dim3(64), 0, s, Q, c->qwork.as<double>(),
                      c->xb.as<double>(), c->rec.as<double>(), x_out);
