@@ -845,7 +845,7 @@ __global__ __launch_bounds__(solve_threads<NP>()) void k_big_solve(BigArgs A, co
 }
 
 // ------------------------------------------------------------------------------------
-// Batched blocked LDL^T of the side systems (CPL = false, NP % 64 == 0).  The systems of
+// Batched blocked LDL^T of the side systems (CPL = false; NP % 64 != 0 ends in a narrower panel).  The systems of
 // a chunk are factored together, one launch pair per 64-column panel, so thousands of
 // independent workgroups keep every CU's memory pipeline busy -- the persistent
 // one-workgroup-per-system kernel above spends most of its time waiting on its own
@@ -919,13 +919,14 @@ __device__ __forceinline__ SideSys<M, NP> side_sys(const BigArgs& A, int code, c
   return S;
 }
 
-// diagonal block of panel c0: A - L[c0:c0+64, :c0] D L[c0:c0+64, :c0]^T (lower tiles
+// diagonal block of panel c0 (NBE = 64 columns, or NP's remainder for the last panel,
+// identity-padded to 64): A - L[c0:c0+NBE, :c0] D L[c0:c0+NBE, :c0]^T (lower tiles
 // (rt, ct <= rt); wave w takes k-steps w, w + 4, ... through a register ring), stored
 // into the slab's W area for k_bs_dfac
-template <class M, int NP>
+template <class M, int NP, int NBE>
 __global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __restrict__ list, int w0, int c0,
                                                  const double* __restrict__ qwork, double* __restrict__ lscr) {
-  constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, PD = 4;
+  constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, PD = 4, NT = NBE / 16;
   __shared__ double T[NB * LT];
   const int w = w0 + (int)blockIdx.x;
   if (w >= list[0]) return;
@@ -937,20 +938,20 @@ __global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __res
 #pragma unroll
   for (int i = 0; i < NB * NB / 256; ++i) {
     const int e = tid + 256 * i, r = e >> 6, cc = e & 63;
-    T[r * LT + cc] = cc <= r ? H.at(c0 + r, c0 + cc) : 0.0;
+    T[r * LT + cc] = (r < NBE && cc < NBE) ? (cc <= r ? H.at(c0 + r, c0 + cc) : 0.0) : (r == cc ? 1.0 : 0.0);
   }
   d4_t acc[10];
 #pragma unroll
   for (int t = 0; t < 10; ++t) acc[t] = d4_t{0.0, 0.0, 0.0, 0.0};
   const int nst = c0 >> 2;
   const int nmy = nst > wave ? (nst - wave + 3) >> 2 : 0;
-  double ra[PD][4], rd[PD];
-  auto ld = [&](int m, double (&a)[4], double& d) {
+  double ra[PD][NT], rd[PD];
+  auto ld = [&](int m, double (&a)[NT], double& d) {
     const int k = 4 * (wave + 4 * m) + kl;
     const double* __restrict__ Lc = Ls + (int64_t)k * LDR + c0;
     d = dd[k];
 #pragma unroll
-    for (int rt = 0; rt < 4; ++rt) a[rt] = Lc[16 * rt + ml];
+    for (int rt = 0; rt < NT; ++rt) a[rt] = Lc[16 * rt + ml];
   };
 #pragma unroll
   for (int d = 0; d < PD; ++d)
@@ -961,7 +962,7 @@ __global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __res
       if (m0 + d < nmy) {
         int t = 0;
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
+        for (int rt = 0; rt < NT; ++rt) {
           const double a = -ra[d][rt] * rd[d];
 #pragma unroll
           for (int ct = 0; ct <= rt; ++ct, ++t) acc[t] = mfma4(a, ra[d][ct], acc[t]);
@@ -976,7 +977,7 @@ __global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __res
     if (wave == wv) {
       int t = 0;
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt)
+      for (int rt = 0; rt < NT; ++rt)
 #pragma unroll
         for (int ct = 0; ct <= rt; ++ct, ++t)
 #pragma unroll
@@ -992,7 +993,7 @@ __global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __res
 // of L11^-1 by forward substitution), stored transposed and XOR-swizzled,
 // Wt[n][j ^ 4 (n & 7)] = W[j][n], so k_bs_trail's B-operand reads from its linear LDS copy
 // are two-way at most
-template <class M, int NP>
+template <class M, int NP, int NBE>
 __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list, int w0, int c0,
                                                 double* __restrict__ lscr) {
   constexpr int LDR = NP + 16, NB = kBsNB;
@@ -1016,12 +1017,12 @@ __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list
   double dl = a[0];
 #pragma unroll
   for (int t = 1; t < NB; ++t) dl = t == lane ? a[t] : dl;
-  dd[c0 + lane] = dl;
+  if (lane < NBE) dd[c0 + lane] = dl;
   const double rdl = 1.0 / dl;
 #pragma unroll
   for (int t = 0; t < NB; ++t) {                            // a[t] becomes L11[lane][t], t < lane
     a[t] = t < lane ? a[t] * readlane_dbl(rdl, t) : 0.0;
-    if (t < lane) Ls[(int64_t)(c0 + t) * LDR + c0 + lane] = a[t];
+    if (t < lane && lane < NBE) Ls[(int64_t)(c0 + t) * LDR + c0 + lane] = a[t];
   }
   // lane j: column j of L11^-1 (x_m = 0 for m < j)
   double x[NB];
@@ -1036,11 +1037,11 @@ __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list
   for (int n = 0; n < NB; ++n) W[n * NB + (lane ^ (4 * (n & 7)))] = x[n] * readlane_dbl(rdl, n);
 }
 
-template <class M, int NP>
+template <class M, int NP, int NBE>
 __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __restrict__ list, int w0, int c0,
                                                   int tpb, const double* __restrict__ qwork,
                                                   double* __restrict__ lscr) {
-  constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, MG = kBsMG, PDT = 5;
+  constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, MG = kBsMG, PDT = 5, NT = NBE / 16;
   __shared__ double Pw[4][16 * LT];
   __shared__ double Ws[NB * NB];
   const int sys = (int)blockIdx.x / tpb, grp = (int)blockIdx.x - sys * tpb;
@@ -1055,28 +1056,28 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
   for (int i = 0; i < NB * NB / 512; ++i)
     __builtin_amdgcn_global_load_lds((glb_vp)(W + 2 * (i * 256 + tid)), (lds_vp)(Ws + 2 * (i * 256 + wave * 64)), 16,
                                      0, 0);
-  const int R0 = c0 + NB + 16 * MG * (4 * grp + wave);     // first row of this wave's tiles
+  const int R0 = c0 + NBE + 16 * MG * (4 * grp + wave);    // first row of this wave's tiles
   const bool active = R0 < LDR;
   const int ng = (LDR - R0) / 16 < MG ? (LDR - R0) / 16 : MG;
   const SideSys<M, NP> H = side_sys<M, NP>(A, list[1 + w], qwork);
-  d4_t acc[MG][4];
+  d4_t acc[MG][NT];
 #pragma unroll
   for (int m = 0; m < MG; ++m)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[m][ct][r] = H.at(R0 + 16 * m + kl + 4 * r, c0 + 16 * ct + ml);
   // panel update: k-steps (4 factored columns each) through a ring of PDT register slots
   const int nst = active ? c0 >> 2 : 0;
-  double ra[PDT][MG], rb[PDT][4], rd[PDT];
-  auto ld = [&](int st, double (&a)[MG], double (&b)[4], double& d) {
+  double ra[PDT][MG], rb[PDT][NT], rd[PDT];
+  auto ld = [&](int st, double (&a)[MG], double (&b)[NT], double& d) {
     const int k = 4 * st + kl;
     const double* __restrict__ Lc = Ls + (int64_t)k * LDR;
     d = dd[k];
 #pragma unroll
     for (int m = 0; m < MG; ++m) a[m] = Lc[R0 + 16 * m + ml];     // rows past LDR: never used (m >= ng)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) b[ct] = Lc[c0 + 16 * ct + ml];
+    for (int ct = 0; ct < NT; ++ct) b[ct] = Lc[c0 + 16 * ct + ml];
   };
 #pragma unroll
   for (int d = 0; d < PDT; ++d)
@@ -1089,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
         for (int m = 0; m < MG; ++m) {
           const double a = -ra[d][m] * rd[d];
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[m][ct] = mfma4(a, rb[d][ct], acc[m][ct]);
+          for (int ct = 0; ct < NT; ++ct) acc[m][ct] = mfma4(a, rb[d][ct], acc[m][ct]);
         }
         if (s0 + d + PDT < nst) ld(s0 + d + PDT, ra[d], rb[d], rd[d]);
       }
@@ -1103,29 +1104,29 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
   for (int m = 0; m < MG; ++m) {
     if (m >= ng) continue;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
       for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = acc[m][ct][r];
     wave_lds_sync();
-    double pa[NB / 4];
+    double pa[4 * NT];
 #pragma unroll
-    for (int s = 0; s < NB / 4; ++s) pa[s] = P[ml * LT + 4 * s + kl];
-    d4_t o[4];
+    for (int s = 0; s < 4 * NT; ++s) pa[s] = P[ml * LT + 4 * s + kl];
+    d4_t o[NT];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
+    for (int ct = 0; ct < NT; ++ct) {
       o[ct] = d4_t{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4 * ct + 4; ++s) o[ct] = mfma4(pa[s], Ws[(16 * ct + ml) * NB + ((4 * s + kl) ^ (4 * (ml & 7)))], o[ct]);
     }
     wave_lds_sync();
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
       for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = o[ct][r];
     wave_lds_sync();
     const int Rm = R0 + 16 * m;
 #pragma unroll
-    for (int i = 0; i < NB / 4; ++i) Ls[(int64_t)(c0 + kl + 4 * i) * LDR + Rm + ml] = P[ml * LT + kl + 4 * i];
+    for (int i = 0; i < NBE / 4; ++i) Ls[(int64_t)(c0 + kl + 4 * i) * LDR + Rm + ml] = P[ml * LT + kl + 4 * i];
     wave_lds_sync();
   }
 }
@@ -1152,32 +1153,34 @@ __global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __res
   // block's operands (the triangle and the GEMV columns) are loaded behind the current one.
   constexpr int WPT = BW * BW / kST > 0 ? BW * BW / kST : 1;   // triangle entries per thread
   auto fetch = [&](int b0, double (&lv)[CPT][BW], double (&wl)[WPT]) {
+    const int bw = NP - b0 < BW ? NP - b0 : BW;   // the last block of an NP % BW != 0 system
 #pragma unroll
     for (int cc = 0; cc < CPT; ++cc) {
       const int c = tid + cc * kST;
 #pragma unroll
-      for (int t = 0; t < BW; ++t) lv[cc][t] = c < b0 ? Ls[(int64_t)c * LDR + b0 + t] : 0.0;
+      for (int t = 0; t < BW; ++t) lv[cc][t] = (c < b0 && t < bw) ? Ls[(int64_t)c * LDR + b0 + t] : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < WPT; ++k) {          // W11[c][t] = L[b0 + t][b0 + c], t > c
       const int e = tid + k * kST, cc = e / BW, t = e - cc * BW;
-      wl[k] = (e < BW * BW && t > cc) ? Ls[(int64_t)(b0 + cc) * LDR + b0 + t] : 0.0;
+      wl[k] = (e < BW * BW && t > cc && t < bw) ? Ls[(int64_t)(b0 + cc) * LDR + b0 + t] : 0.0;
     }
   };
   auto process = [&](int b0, const double (&lv)[CPT][BW], const double (&wl)[WPT]) {
+    const int bw = NP - b0 < BW ? NP - b0 : BW;
 #pragma unroll
     for (int k = 0; k < WPT; ++k)
       if (tid + k * kST < BW * BW) W11[tid + k * kST] = wl[k];
     __syncthreads();
     if (wave == 0) {
-      double val = lane < BW ? xs[b0 + lane] : 0.0;
+      double val = lane < bw ? xs[b0 + lane] : 0.0;
       const double* __restrict__ Wc = W11 + (lane < BW ? lane : 0) * BW;
 #pragma unroll
       for (int t = BW - 1; t >= 0; --t) {
         const double xt = readlane_dbl(val, t);
         if (lane < t) val = fma(-Wc[t], xt, val);
       }
-      if (lane < BW) xs[b0 + lane] = val;
+      if (lane < bw) xs[b0 + lane] = val;
     }
     __syncthreads();
 #pragma unroll
@@ -1186,7 +1189,7 @@ __global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __res
       if (c < b0) {
         double s = xs[c];
 #pragma unroll
-        for (int t = 0; t < BW; ++t) s = fma(-lv[cc][t], xs[b0 + t], s);
+        for (int t = 0; t < BW; ++t) s = fma(-lv[cc][t], t < bw ? xs[b0 + t] : 0.0, s);
         xs[c] = s;
       }
     }
@@ -1595,9 +1598,26 @@ hipError_t launch_solve(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int
 
 // side systems through the batched panel kernels, chunks of <= kBsScratch bytes of slabs;
 // list[0] (the device-side count) bounds every launch, max_sys only sizes them
+template <class M, int NP, int NBE>
+hipError_t launch_bs_panel(fia_ctx* c, const BigArgs& A, int64_t w0, int64_t n, int c0, const int32_t* list,
+                           hipStream_t s) {
+  hipLaunchKernelGGL((k_bs_dupd<M, NP, NBE>), dim3((unsigned)n), dim3(256), 0, s, A, list, (int)w0, c0,
+                     c->qwork.as<double>(), c->lscr.as<double>());
+  FIA_HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL((k_bs_dfac<M, NP, NBE>), dim3((unsigned)n), dim3(64), 0, s, list, (int)w0, c0,
+                     c->lscr.as<double>());
+  FIA_HIP_TRY(hipGetLastError());
+  const int tiles = (NP + 16 - c0 - NBE) / 16;
+  const int tpb = (tiles + 4 * kBsMG - 1) / (4 * kBsMG);
+  hipLaunchKernelGGL((k_bs_trail<M, NP, NBE>), dim3((unsigned)(n * tpb)), dim3(256), 0, s, A, list, (int)w0, c0, tpb,
+                     c->qwork.as<double>(), c->lscr.as<double>());
+  return hipGetLastError();
+}
+
 template <class M, int NP>
 hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int32_t* list, hipStream_t s) {
-  static_assert(NP % kBsNB == 0, "batched solve needs whole panels");
+  static_assert(NP % 16 == 0, "side blocks are whole 16-column tiles");
+  constexpr int kLast = NP % kBsNB == 0 ? kBsNB : NP % kBsNB;   // last panel's width
   if (max_sys <= 0) return hipSuccess;
   constexpr int64_t slab = bs_slab<NP>();
   static const int64_t scratch = getenv("FIA_BS_SCRATCH_MB") ? atoll(getenv("FIA_BS_SCRATCH_MB")) << 20 : kBsScratch;
@@ -1607,17 +1627,10 @@ hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, c
   for (int64_t w0 = 0; w0 < max_sys; w0 += S) {
     const int64_t n = max_sys - w0 < S ? max_sys - w0 : S;
     for (int c0 = 0; c0 < NP; c0 += kBsNB) {
-      hipLaunchKernelGGL((k_bs_dupd<M, NP>), dim3((unsigned)n), dim3(256), 0, s, A, list, (int)w0, c0,
-                         c->qwork.as<double>(), c->lscr.as<double>());
-      FIA_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL((k_bs_dfac<M, NP>), dim3((unsigned)n), dim3(64), 0, s, list, (int)w0, c0,
-                         c->lscr.as<double>());
-      FIA_HIP_TRY(hipGetLastError());
-      const int tiles = (NP + 16 - c0 - kBsNB) / 16;
-      const int tpb = (tiles + 4 * kBsMG - 1) / (4 * kBsMG);
-      hipLaunchKernelGGL((k_bs_trail<M, NP>), dim3((unsigned)(n * tpb)), dim3(256), 0, s, A, list, (int)w0, c0, tpb,
-                         c->qwork.as<double>(), c->lscr.as<double>());
-      FIA_HIP_TRY(hipGetLastError());
+      if (NP - c0 >= kBsNB)
+        FIA_HIP_TRY((launch_bs_panel<M, NP, kBsNB>(c, A, w0, n, c0, list, s)));
+      else
+        FIA_HIP_TRY((launch_bs_panel<M, NP, kLast>(c, A, w0, n, c0, list, s)));
     }
     hipLaunchKernelGGL((k_bs_back<M, NP>), dim3((unsigned)n), dim3(512), 0, s, A, list, (int)w0,
                        c->qwork.as<double>(), c->lscr.as<double>(), c->xb.as<double>(), c->rec.as<double>());
@@ -1651,14 +1664,10 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   hipLaunchKernelGGL(k_big_prologue<M>, dim3(grid_cap(Q, 1 << 20)), dim3(256), 0, s, A, Q, c->qwork.as<double>(),
                      c->syslist.as<int32_t>(), c->cpllist.as<int32_t>());
   FIA_HIP_TRY(hipGetLastError());
-  if constexpr (NPs % kBsNB == 0) {
-    if (!getenv("FIA_BIG_SOLVE_PERSISTENT"))
-      FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
-    else
-      FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
-  } else {
+  if (!getenv("FIA_BIG_SOLVE_PERSISTENT"))
+    FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+  else
     FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
-  }
   FIA_HIP_TRY((launch_solve<M, 2 * NPs, true>(c, A, Q, c->cpllist.as<int32_t>(), s)));
   hipLaunchKernelGGL(k_big_finish<M>, dim3(grid_cap(Q, 1 << 20)), dim3(64), 0, s, Q, c->qwork.as<double>(),
                      c->xb.as<double>(), c->rec.as<double>(), x_out);
