@@ -1413,6 +1413,208 @@ __global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
 }
 
 // ------------------------------------------------------------------------------------
+// Entity-shared scoring on the f64 matrix cores (same work items, same outputs and
+// top-K candidate slots as k_big_score, blocks of kBigMfmaQB queries).  A workgroup
+// takes one work item; wave h is scoring pass h (ratings [64 h, 64 h + 64) of the
+// chunk, four 16-rating tiles).  Per tile the scores are one 16 x 16 MFMA product
+// over the dotted length KD (MF: x_emb . emb_other; NCF: x_mlp . g_mlp,j then
+// (W3g * x_gmf) . gmf_other): A = the block's query vectors (LDS, k-major), B = the
+// tile's rating vectors streamed from HBM, four consecutive coordinates per lane
+// (full 128-B lines per row).  Lane (m, g) ends with the scores of rating m against
+// queries g, g + 4, g + 8, g + 12, so each influence store is four 128-B segments.
+// ------------------------------------------------------------------------------------
+constexpr int kBigMfmaQB = 16;
+
+template <class M>
+constexpr int score_kd() { return M::ncf ? 2 * M::K : M::K; }
+
+template <class M>
+__global__ __launch_bounds__(256) void k_big_score_mfma(
+    BigArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
+    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  constexpr int K = M::K, KD = score_kd<M>(), QB = kBigMfmaQB, XS = QB + 1, NPASS = kScoreRows;
+  static_assert(NPASS == 4, "one wave per scoring pass");
+  __shared__ double Xs[KD * XS];       // Xs[k * XS + j]: coordinate k of query j's vector
+  __shared__ double Qs[QB][6];         // 1/n, c_q, x.v, r-hat, dup_other, x_bias (MF)
+  __shared__ int64_t Bs[QB][3];        // influence offset, candidate chunk, position offset
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
+  const int64_t n_items = wstart[nE];
+  for (int64_t wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
+    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+    const int sd = g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(g - A.U) : g;
+    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
+    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int len = rem < kChunk ? (int)rem : kChunk;
+    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
+    const int64_t gn = gstart[g + 1] - gb;
+    const int nq = gn < QB ? (int)gn : QB;
+    __syncthreads();                   // the previous item's LDS is consumed
+    for (int t = tid; t < KD * QB; t += 256) {
+      const int j = t / KD, k = t - j * KD;
+      double v = 0.0;
+      if (j < nq) v = rec[(int64_t)gq[gb + j] * M::R + 8 + sd * M::SB + k];
+      Xs[k * XS + j] = v;
+    }
+    if (tid < QB) {
+      const int32_t q = gq[gb + (tid < nq ? tid : nq - 1)];
+      const double* __restrict__ R = rec + (int64_t)q * M::R;
+      const double* __restrict__ S = R + 8 + sd * M::SB;
+      Qs[tid][0] = R[0];
+      Qs[tid][1] = R[1];
+      Qs[tid][2] = R[2];
+      Qs[tid][3] = R[3];
+      Qs[tid][4] = M::ncf ? S[2 * K] : S[K + 1];
+      Qs[tid][5] = M::ncf ? 0.0 : S[K];
+      const int64_t* qb = qbase + 4 * (int64_t)q;
+      Bs[tid][0] = qb[sd] + (int64_t)cidx * kChunk;
+      Bs[tid][1] = qb[2 + sd] + cidx;
+      Bs[tid][2] = sd ? qb[1] - qb[0] : 0;
+    }
+    __syncthreads();
+    // this wave's four tiles: rating idx = 64 wave + 16 t + m
+    int32_t o[4], rw[4];
+    float y[4];
+    double ej[4];
+    bool ok[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int idx = 64 * wave + 16 * t + ml;
+      ok[t] = idx < len;
+      const int li = ok[t] ? idx : 0;
+      o[t] = A.other[sd][lb + li];
+      rw[t] = A.row[sd][lb + li];
+      y[t] = A.rating[sd][lb + li];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) ej[t] = A.resid[rw[t]];
+    d4_t acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = d4_t{0.0, 0.0, 0.0, 0.0};
+    // k-groups of 16 coordinates: lane (m, g) holds coordinates 16 G + 4 g + i, i < 4, of
+    // rating m; MFMA step i of the group uses coordinate 16 G + 4 g + i on both sides
+    auto group = [&](int G, const double (&b)[4][4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double a = Xs[(16 * G + 4 * kl + i) * XS + ml];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = mfma4(a, b[t][i], acc[t]);
+      }
+    };
+    if constexpr (M::ncf) {
+      // x_mlp . g_mlp,j: g_mlp rows of this side (fp64)
+      const double* __restrict__ gmr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) gmr[t] = A.gm[sd] + (int64_t)rw[t] * K + 4 * kl;
+      double bA[4][4], bB[4][4];
+      auto ldg = [&](int G, double (&b)[4][4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const double2 u0 = *reinterpret_cast<const double2*>(gmr[t] + 16 * G);
+          const double2 u1 = *reinterpret_cast<const double2*>(gmr[t] + 16 * G + 2);
+          b[t][0] = u0.x; b[t][1] = u0.y; b[t][2] = u1.x; b[t][3] = u1.y;
+        }
+      };
+      ldg(0, bA);
+      for (int G = 0; G < K / 16; G += 2) {
+        ldg(G + 1, bB);
+        group(G, bA);
+        if (G + 2 < K / 16) ldg(G + 2, bA);
+        group(G + 1, bB);
+      }
+    }
+    {
+      // (MF: x_emb, NCF: W3g * x_gmf) . the other side's embedding row (fp32)
+      constexpr int KOFF = M::ncf ? K : 0;
+      const float* __restrict__ T = M::ncf ? (sd == 0 ? A.t[3] : A.t[2]) : (sd == 0 ? A.t[1] : A.t[0]);
+      const float* __restrict__ er[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) er[t] = T + (int64_t)o[t] * K + 4 * kl;
+      float4 fA[4], fB[4];
+      auto lde = [&](int G, float4 (&f)[4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) f[t] = *reinterpret_cast<const float4*>(er[t] + 16 * G);
+      };
+      auto grp = [&](int G, const float4 (&f)[4]) {
+        double b[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          b[t][0] = f[t].x; b[t][1] = f[t].y; b[t][2] = f[t].z; b[t][3] = f[t].w;
+        }
+        group(KOFF / 16 + G, b);
+      };
+      lde(0, fA);
+      for (int G = 0; G < K / 16; G += 2) {
+        lde(G + 1, fB);
+        grp(G, fA);
+        if (G + 2 < K / 16) lde(G + 2, fA);
+        grp(G + 1, fB);
+      }
+    }
+    // influence of rating m against queries kl + 4 r
+    double la[4][4];   // [r][t] top-K keys
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = kl + 4 * r;
+      const double inv_n = Qs[j][0], cq = Qs[j][1], xv = Qs[j][2], rhat = Qs[j][3], dup = Qs[j][4], xb = Qs[j][5];
+      const int64_t obj = Bs[j][0];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        double ss = acc[t][r] + xb, ee = ej[t];
+        if ((double)o[t] == dup) { ee = rhat - (double)y[t]; ss = xv; }
+        const double infl = (2.0 * ee * ss + cq) * inv_n;
+        const int idx = 64 * wave + 16 * t + ml;
+        if (ok[t] && j < nq) {
+          if (influence) influence[obj + idx] = infl;
+          if (rel_idx) rel_idx[obj + idx] = (int64_t)rw[t];
+        }
+        acc[t][r] = infl;
+        la[r][t] = ok[t] ? topk_key(infl) : -2.0;
+      }
+    }
+    if (K_top > 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = kl + 4 * r;
+        const int64_t cbj = Bs[j][1], poj = Bs[j][2];
+        double pa = INFINITY;
+        int pp = -1;
+        for (int tt = 0; tt < K_top; ++tt) {
+          double ba = -2.0, bv = 0.0;
+          int bp = 0x7fffffff;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int lp = ok[t] ? cidx * kChunk + 64 * wave + 16 * t + ml : -1;
+            if (lp >= 0 && better(pa, pp, la[r][t], lp) && better(la[r][t], lp, ba, bp)) {
+              ba = la[r][t];
+              bp = lp;
+              bv = acc[t][r];
+            }
+          }
+#pragma unroll
+          for (int off = 8; off > 0; off >>= 1) {   // within the 16 lanes of query j
+            const double oa = __shfl_xor(ba, off);
+            const int op = __shfl_xor(bp, off);
+            const double ov = __shfl_xor(bv, off);
+            if (better(oa, op, ba, bp)) { ba = oa; bp = op; bv = ov; }
+          }
+          if (ml == 0 && j < nq) {
+            const bool okk = ba > -1.5;
+            const int64_t slot = (cbj * NPASS + wave) * K_top + tt;
+            cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+            cand_val[slot] = okk ? bv : NAN;
+          }
+          pa = ba;
+          pp = bp;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
 BigArgs make_big_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
@@ -1656,7 +1858,8 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   const BigArgs A = make_big_args(c, qu, qi);
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, true, s));
-  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, kBigQueryBlock, s));
+  const bool mfma_score = !getenv("FIA_BIG_SCORE_VALU");
+  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, mfma_score ? kBigMfmaQB : kBigQueryBlock, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   FIA_HIP_TRY(hipMemsetAsync(c->syslist.ptr, 0, sizeof(int32_t), s));
@@ -1674,10 +1877,16 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
   phase_begin(c, 2, s);
-  hipLaunchKernelGGL(k_big_score<M>, dim3(grid_cap((max_chunks + SW - 1) / SW, 8192)), dim3(64 * SW), 0, s, A,
-                     c->p.U + c->p.I, c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
-                     c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                     c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+  if (mfma_score)
+    hipLaunchKernelGGL(k_big_score_mfma<M>, dim3(grid_cap(max_chunks, 8192)), dim3(256), 0, s, A, c->p.U + c->p.I,
+                       c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
+                       c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
+                       c->cand_val.as<double>());
+  else
+    hipLaunchKernelGGL(k_big_score<M>, dim3(grid_cap((max_chunks + SW - 1) / SW, 8192)), dim3(64 * SW), 0, s, A,
+                       c->p.U + c->p.I, c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                       c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);
   if (K > 0) {
