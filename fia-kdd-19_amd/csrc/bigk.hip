@@ -845,26 +845,30 @@ __global__ __launch_bounds__(solve_threads<NP>()) void k_big_solve(BigArgs A, co
 }
 
 // ------------------------------------------------------------------------------------
-// Batched blocked LDL^T of the side systems (CPL = false; NP % 64 != 0 ends in a narrower panel).  The systems of
-// a chunk are factored together, one launch pair per 64-column panel, so thousands of
-// independent workgroups keep every CU's memory pipeline busy -- the persistent
-// one-workgroup-per-system kernel above spends most of its time waiting on its own
-// panel chain.  Per system slab: L (column-major, LDR = NP + 16 rows, row NP the
-// right-hand side v^T), d (NP) and W = (D11 L11^T)^-1 of the current panel (64 x 64).
+// Batched blocked LDL^T of the side systems (CPL = false).  The systems of a chunk are
+// factored together, three launches per 64-column panel (NP % 64 != 0 ends in a
+// narrower one), so thousands of independent workgroups keep every CU's memory
+// pipeline busy -- the persistent one-workgroup-per-system kernel above spends most of
+// its time waiting on its own panel chain.  Per system slab: L (column-major,
+// LDR = NP + 16 rows, row NP the right-hand side v^T), d (NP), the current panel's
+// diagonal block (64 x 64) and L11^-1 of every panel (64 x 64 each).
 //   k_bs_dupd : the panel's diagonal block A - L D L^T (MFMA, k-steps split over four
 //               waves);
-//   k_bs_dfac : its LDL^T in one wave (readlane broadcasts), W by forward substitution
-//               (lane j: column j of L11^-1);
+//   k_bs_dfac : its LDL^T in one wave (readlane broadcasts), L11^-1 by forward
+//               substitution (lane j: column j);
 //   k_bs_trail: per 16-row tile below the block, the panel update (MFMA, L streamed)
-//               and the triangular solve as one more MFMA product, P W, stored as L;
-//   k_bs_back : L^T x = y (y = row NP of L) and the scoring record.
+//               and the triangular solve as one more MFMA product, P L11^-T D^-1;
+//   k_bs_back : L^T x = y (y = row NP of L) by 64-column blocks from the end, each block's
+//               triangle as a product with its stored L11^-1, and the scoring record.
 // ------------------------------------------------------------------------------------
 constexpr int kBsNB = 64;                          // panel width
 constexpr int kBsMG = 2;                           // row tiles per k_bs_trail wave
 constexpr int64_t kBsScratch = (int64_t)8 << 30;   // bytes of factor slabs per chunk
 
 template <int NP>
-__host__ __device__ constexpr int64_t bs_slab() { return (int64_t)(NP + 16) * NP + NP + kBsNB * kBsNB; }
+__host__ __device__ constexpr int64_t bs_slab() {   // L, d, W, then L11^-1 of every panel
+  return (int64_t)(NP + 16) * NP + NP + kBsNB * kBsNB + (int64_t)((NP + kBsNB - 1) / kBsNB) * kBsNB * kBsNB;
+}
 
 // wave-local LDS hand-off: a wave's LDS operations complete in order; this only keeps
 // the compiler from moving them across the exchange
@@ -989,10 +993,11 @@ __global__ __launch_bounds__(256) void k_bs_dupd(BigArgs A, const int32_t* __res
 }
 
 // LDL^T of the updated diagonal block (one wave per system; lane r owns row r, readlane
-// broadcasts, no LDS), L11 and d into the slab, then W = L11^-T D^-1 (lane j: column j
-// of L11^-1 by forward substitution), stored transposed and XOR-swizzled,
-// Wt[n][j ^ 4 (n & 7)] = W[j][n], so k_bs_trail's B-operand reads from its linear LDS copy
-// are two-way at most
+// broadcasts, no LDS), L11 and d into the slab, then L11^-1 (lane j: column j by forward
+// substitution) into the panel's X slot, XOR-swizzled: Xp[n][j ^ 4 (n & 7)] = (L11^-1)[n][j],
+// so k_bs_trail's B-operand reads from its linear LDS copy are two-way at most.  The
+// triangular solve needs W = L11^-T D^-1, i.e. W[j][n] = Xp[n][j] / d_n: k_bs_trail scales
+// its product's columns; k_bs_back uses L11^-T itself.
 template <class M, int NP, int NBE>
 __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list, int w0, int c0,
                                                 double* __restrict__ lscr) {
@@ -1033,8 +1038,9 @@ __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list
     for (int m = 0; m < i; ++m) s = fma(-readlane_dbl(a[m], i), x[m], s);
     x[i] = s;
   }
+  double* __restrict__ Xp = W + NB * NB + (int64_t)(c0 / NB) * NB * NB;
 #pragma unroll
-  for (int n = 0; n < NB; ++n) W[n * NB + (lane ^ (4 * (n & 7)))] = x[n] * readlane_dbl(rdl, n);
+  for (int n = 0; n < NB; ++n) Xp[n * NB + (lane ^ (4 * (n & 7)))] = x[n];
 }
 
 template <class M, int NP, int NBE>
@@ -1050,8 +1056,8 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
   double* __restrict__ Ls = lscr + (int64_t)sys * bs_slab<NP>();
   const double* __restrict__ dd = Ls + (int64_t)LDR * NP;
-  const double* __restrict__ W = dd + NP;
-  // W of this panel (k_bs_dfac) into LDS by DMA, landing while the panel update runs
+  const double* __restrict__ W = dd + NP + NB * NB + (int64_t)(c0 / NB) * NB * NB;   // this panel's L11^-1
+  // L11^-1 of this panel (k_bs_dfac) into LDS by DMA, landing while the panel update runs
 #pragma unroll
   for (int i = 0; i < NB * NB / 512; ++i)
     __builtin_amdgcn_global_load_lds((glb_vp)(W + 2 * (i * 256 + tid)), (lds_vp)(Ws + 2 * (i * 256 + wave * 64)), 16,
@@ -1098,7 +1104,11 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
   }
   __syncthreads();   // W landed
   if (!active) return;
-  // triangular solve: L[rows][panel] = P W (W upper triangular), through this wave's LDS tile
+  // triangular solve: L[rows][panel] = P L11^-T D^-1 (upper triangular), through this
+  // wave's LDS tile; column n of the product scaled by 1 / d_n
+  double rdn[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) rdn[ct] = 1.0 / dd[c0 + 16 * ct + ml];
   double* __restrict__ P = Pw[wave];
 #pragma unroll
   for (int m = 0; m < MG; ++m) {
@@ -1122,7 +1132,7 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = o[ct][r];
+      for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = o[ct][r] * rdn[ct];
     wave_lds_sync();
     const int Rm = R0 + 16 * m;
 #pragma unroll
@@ -1135,10 +1145,8 @@ template <class M, int NP>
 __global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __restrict__ list, int w0,
                                                  const double* __restrict__ qwork, double* __restrict__ lscr,
                                                  double* __restrict__ xb, double* __restrict__ rec) {
-  constexpr int K = M::K, NPs = M::NPs, Ds = M::Ds, LDR = NP + 16, kST = 512, kSW = kST / 64;
-  constexpr int CPT = (NP + kST - 1) / kST, BW = CPT == 1 ? 32 : 16;
-  __shared__ double xs[NP];
-  __shared__ double W11[BW * BW];
+  constexpr int K = M::K, NPs = M::NPs, Ds = M::Ds, LDR = NP + 16, kST = 512, kSW = kST / 64, NB = kBsNB;
+  __shared__ double xs[NP + NB];       // zero past NP: a partial last block reads it unguarded
   __shared__ double red[64];
   const int w = w0 + (int)blockIdx.x;
   if (w >= list[0]) return;
@@ -1147,64 +1155,43 @@ __global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __res
   const int sd = code & 1;
   const double* __restrict__ qw = qwork + q * M::QW;
   const double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * bs_slab<NP>();
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // L^T x = y, y_c = L[NP][c]; BW-column blocks from the end: a one-wave triangle per
-  // block (staged in W11), then the GEMV update of the earlier entries.  The next
-  // block's operands (the triangle and the GEMV columns) are loaded behind the current one.
-  constexpr int WPT = BW * BW / kST > 0 ? BW * BW / kST : 1;   // triangle entries per thread
-  auto fetch = [&](int b0, double (&lv)[CPT][BW], double (&wl)[WPT]) {
-    const int bw = NP - b0 < BW ? NP - b0 : BW;   // the last block of an NP % BW != 0 system
-#pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) {
-      const int c = tid + cc * kST;
-#pragma unroll
-      for (int t = 0; t < BW; ++t) lv[cc][t] = (c < b0 && t < bw) ? Ls[(int64_t)c * LDR + b0 + t] : 0.0;
+  const double* __restrict__ X = Ls + (int64_t)LDR * NP + NP + NB * NB;
+  const int tid = threadIdx.x;
+  // L^T x = y, y_c = L[NP][c].  Per 64-column block b from the end: x_b = L_bb^-T z_b with
+  // the panel's stored inverse (z_b: y_b after the later blocks' updates), then
+  // z_c -= sum_t L[b0 + t][c] x_b[t] for every earlier c.  One global round trip per block.
+  for (int c = tid; c < NP + NB; c += kST) xs[c] = c < NP ? Ls[(int64_t)c * LDR + NP] : 0.0;
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int b0 = ((NP - 1) / NB) * NB; b0 >= 0; b0 -= NB) {
+    const int bw = NP - b0 < NB ? NP - b0 : NB;
+    if (tid < bw) {
+      // (L^-T)[c][n] = (L^-1)[n][c], zero for n < c and (identity padding) for n >= bw
+      const double* __restrict__ Xb = X + (int64_t)(b0 / NB) * NB * NB;
+      double xc = 0.0;
+#pragma unroll 8
+      for (int n = 0; n < NB; ++n) xc = fma(Xb[n * NB + (tid ^ (4 * (n & 7)))], xs[b0 + n], xc);
+      __builtin_amdgcn_wave_barrier();   // (wave 0 only) every lane has read the block's z
+      xs[b0 + tid] = xc;
     }
-#pragma unroll
-    for (int k = 0; k < WPT; ++k) {          // W11[c][t] = L[b0 + t][b0 + c], t > c
-      const int e = tid + k * kST, cc = e / BW, t = e - cc * BW;
-      wl[k] = (e < BW * BW && t > cc && t < bw) ? Ls[(int64_t)(b0 + cc) * LDR + b0 + t] : 0.0;
-    }
-  };
-  auto process = [&](int b0, const double (&lv)[CPT][BW], const double (&wl)[WPT]) {
-    const int bw = NP - b0 < BW ? NP - b0 : BW;
-#pragma unroll
-    for (int k = 0; k < WPT; ++k)
-      if (tid + k * kST < BW * BW) W11[tid + k * kST] = wl[k];
     __syncthreads();
-    if (wave == 0) {
-      double val = lane < bw ? xs[b0 + lane] : 0.0;
-      const double* __restrict__ Wc = W11 + (lane < BW ? lane : 0) * BW;
+    // z_c -= L[b0:b0+bw][c] . x_b: a column per wave step, lane t on row b0 + t (one
+    // coalesced 512-B read per column), eight columns in flight
+    const double xt = lane < bw ? xs[b0 + lane] : 0.0;
+    for (int c0 = 8 * wave; c0 < b0; c0 += 8 * kSW) {
+      double v[8];
 #pragma unroll
-      for (int t = BW - 1; t >= 0; --t) {
-        const double xt = readlane_dbl(val, t);
-        if (lane < t) val = fma(-Wc[t], xt, val);
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + u;
+        v[u] = (c < b0 && lane < bw) ? Ls[(int64_t)c * LDR + b0 + lane] : 0.0;
       }
-      if (lane < bw) xs[b0 + lane] = val;
-    }
-    __syncthreads();
 #pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) {
-      const int c = tid + cc * kST;
-      if (c < b0) {
-        double s = xs[c];
-#pragma unroll
-        for (int t = 0; t < BW; ++t) s = fma(-lv[cc][t], t < bw ? xs[b0 + t] : 0.0, s);
-        xs[c] = s;
+      for (int u = 0; u < 8; ++u) {
+        const double sum = wsum(v[u] * xt);
+        if (lane == 0 && c0 + u < b0) xs[c0 + u] -= sum;
       }
     }
     __syncthreads();
-  };
-  for (int c = tid; c < NP; c += kST) xs[c] = Ls[(int64_t)c * LDR + NP];
-  double lvA[CPT][BW], lvB[CPT][BW], wlA[WPT], wlB[WPT];
-  const int blast = ((NP - 1) / BW) * BW;
-  fetch(blast, lvA, wlA);
-  for (int b0 = blast; b0 >= 0; b0 -= 2 * BW) {
-    if (b0 - BW >= 0) fetch(b0 - BW, lvB, wlB);
-    process(b0, lvA, wlA);
-    if (b0 - BW < 0) break;
-    if (b0 - 2 * BW >= 0) fetch(b0 - 2 * BW, lvA, wlA);
-    process(b0 - BW, lvB, wlB);
   }
   // padded solution, this side's partial sums and scoring record (as k_big_solve)
   const int32_t u = A.qu[q], i = A.qi[q];
