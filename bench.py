@@ -129,14 +129,17 @@ def load_data(cfg):
 
 
 def score_kernel(cfg, K=1):
-    """The library's scoring kernel for this config (models.hip / bigk.hip schedule choice)."""
+    """The library's scoring kernel for this config (the dispatch in models.hip query_impl /
+    bigk.hip query_big_impl, including their environment switches)."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
-        return "k_big_score"
+        return "k_big_score" if os.environ.get("FIA_BIG_SCORE_VALU") else "k_big_score_mfma"
     if model == "NCF":
         return "k_score_ncf"
     if k <= 16:
         return "k_score_mf"
+    if k in (32, 64) and K <= 1 and not os.environ.get("FIA_NO_MFMA_SCORE"):
+        return "k_score_mf_mfma"
     return "k_score_grouped_mf"
 
 
@@ -312,7 +315,7 @@ def load_traffic(path, config, kernel):
     try:
         tj = json.load(open(path))
         tj = tj.get(config, {}) if "config" not in tj else tj
-        if tj.get("config") == config and tj.get("kernel", "").startswith(kernel):
+        if tj.get("config") == config and tj.get("kernel", "") == kernel:
             return tj
     except Exception:
         return None

@@ -8,12 +8,16 @@ on gfx950 -> doubled; WRITE_SIZE (KB) taken as is."""
 import csv
 import json
 import os
+import re
 import sys
 
 
 def per_dispatch(d, counter, kernel):
+    # whole-name match: the kernel identifier followed by its template or parameter list
+    # (k_score_mf must not pick up k_score_mf_mfma)
+    pat = re.compile(r"\b%s[<(]" % re.escape(kernel))
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
-            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+            if r["Counter_Name"] == counter and pat.search(r["Kernel_Name"])]
     return sum(vals) / len(vals), len(vals)
 
 
