@@ -15,6 +15,7 @@ constexpr int kWave = 64;
 constexpr int kScoreThreads = 256;       // scoring workgroup (4 independent waves)
 constexpr int kScoreRows = 4;            // related ratings per lane and chunk
 constexpr int kChunk = 64 * kScoreRows;  // related ratings per scoring chunk (one wave)
+constexpr int kRunQB = 16;               // queries per item-run block (k_score_mf_run)
 
 // One scoring chunk: <= kChunk consecutive ratings of ONE side (user list or item
 // list) of one query, so every value a wave needs from the query is wave-uniform.
@@ -206,9 +207,12 @@ hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
                          int64_t* offsets, hipStream_t s);
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
                          const int64_t* offsets, int64_t* rel, hipStream_t s);
-// per-query chunk offsets coff (+ chunk descriptors unless offsets_only)
+// per-query chunk offsets coff (+ chunk descriptors unless offsets_only; with `runs` the
+// descriptors are the compacted work list of k_score_mf_run: every user-side chunk, the
+// item-side chunks of run heads only, their count at qbase[4Q])
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr);
+                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr,
+                        bool runs = false);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
 int64_t gram_chunk(int64_t want);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)

@@ -139,7 +139,8 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t Q, const int64_t* __restrict__ uptr,
     const int64_t* __restrict__ iptr, int64_t U, int64_t I, int64_t* __restrict__ out,
     unsigned long long* __restrict__ tstate, unsigned int* __restrict__ tctr, int32_t* __restrict__ flag,
-    const int64_t* __restrict__ offsets, ChunkDesc* __restrict__ cdesc, int32_t* __restrict__ zero_word) {
+    const int64_t* __restrict__ offsets, ChunkDesc* __restrict__ cdesc, int32_t* __restrict__ zero_word,
+    int64_t* __restrict__ qbase, int runs) {
   __shared__ int s_tile;
   __shared__ int64_t s_wave[kScanThreads / 64];
   __shared__ int64_t s_prefix;
@@ -153,12 +154,14 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   // the list bounds (and the output base) stay in registers for the descriptor fill
   // after the look-back, instead of a second dependent qu/qi -> ptr round trip
   int64_t s_ub[kScanItems], s_du[kScanItems], s_ib[kScanItems], s_di[kScanItems], s_base[kScanItems];
+  int s_nq[kScanItems];
   int64_t tsum = 0;
 #pragma unroll
   for (int it = 0; it < kScanItems; ++it) {
     const int64_t q = q0 + it;
     int64_t x = 0;
     s_ub[it] = s_du[it] = s_ib[it] = s_di[it] = s_base[it] = 0;
+    s_nq[it] = 0;
     if (q < Q) {
       if (MODE == 1 && cdesc) s_base[it] = offsets[q];
       const int32_t u = qu[q], i = qi[q];
@@ -167,6 +170,23 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
         const int64_t du = uptr[u + 1] - ub, di = iptr[i + 1] - ib;
         s_ub[it] = ub; s_du[it] = du; s_ib[it] = ib; s_di[it] = di;
         x = MODE == 0 ? du + di : (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
+        if (MODE == 1 && runs) {
+          // packed {chunks (candidate slots) << 31 | work descriptors}: the item-side chunks
+          // are work only for a run head (first query of a run of equal test items, runs cut
+          // at multiples of kRunQB), which scores them for the whole run
+          const bool head = (q % runs) == 0 || qi[q - 1] != i;
+          s_nq[it] = 0;
+          if (head) {
+            int nq = 1;
+            const int lim = runs - (int)(q % runs);
+            for (int j = 1; j < kRunQB; ++j) {
+              const bool same = j < lim && q + j < Q && qi[q + j] == i;
+              nq += (same && nq == j) ? 1 : 0;
+            }
+            s_nq[it] = nq;
+          }
+          x = (x << 31) | ((du + kChunk - 1) / kChunk + (head ? (di + kChunk - 1) / kChunk : 0));
+        }
       } else if (MODE == 0) {
         atomicOr(flag + 1, 1);
       }
@@ -198,10 +218,46 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   }
   __syncthreads();
   int64_t run = s_prefix + wbase + inc - tsum;
+  constexpr int64_t kLo = (1ll << 31) - 1;
 #pragma unroll
   for (int it = 0; it < kScanItems; ++it) {
     const int64_t q = q0 + it;
-    if (q <= Q) out[q] = run;
+    if (q <= Q) out[q] = (MODE == 1 && runs) ? run >> 31 : run;
+    if (MODE == 1 && runs && q == Q) qbase[4 * Q] = run & kLo;     // work descriptors in all
+    if (MODE == 1 && qbase && q < Q) {
+      // per query: {out base user, item}, {candidate slot base user, item} (k_score_mf_run)
+      const int64_t du = s_du[it], cr = runs ? run >> 31 : run;
+      qbase[4 * q + 0] = s_base[it];
+      qbase[4 * q + 1] = s_base[it] + du;
+      qbase[4 * q + 2] = cr;
+      qbase[4 * q + 3] = cr + (du + kChunk - 1) / kChunk;
+    }
+    if (MODE == 1 && runs && cdesc && q < Q && v[it] > 0) {
+      const int64_t ub = s_ub[it], du = s_du[it], ib = s_ib[it], di = s_di[it];
+      int64_t c = run & kLo;
+      const int64_t base = s_base[it];
+      for (int64_t st = 0; st < du; st += kChunk, ++c) {
+        ChunkDesc d;
+        d.list_base = ub + st;
+        d.out_base = base + st;
+        d.q = (int32_t)q;
+        d.pos0 = (int32_t)st;
+        d.len = (int32_t)(du - st < kChunk ? du - st : kChunk);
+        d.side = 0 | (1 << 8);
+        cdesc[c] = d;
+      }
+      if (s_nq[it] > 0)
+        for (int64_t st = 0; st < di; st += kChunk, ++c) {
+          ChunkDesc d;
+          d.list_base = ib + st;
+          d.out_base = base + du + st;
+          d.q = (int32_t)q;
+          d.pos0 = (int32_t)(du + st);
+          d.len = (int32_t)(di - st < kChunk ? di - st : kChunk);
+          d.side = 1 | (s_nq[it] << 8);
+          cdesc[c] = d;
+        }
+    } else
     if (MODE == 1 && cdesc && q < Q && v[it] > 0) {
       const int64_t ub = s_ub[it], du = s_du[it], ib = s_ib[it], di = s_di[it];
       int64_t c = run;
@@ -549,14 +605,15 @@ static hipError_t scan_state(fia_ctx* c, int64_t Q, hipStream_t s) {
 
 template <int MODE>
 static hipError_t launch_query_scan(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* out,
-                                    const int64_t* offsets, ChunkDesc* cdesc, int32_t* zero_word, hipStream_t s) {
+                                    const int64_t* offsets, ChunkDesc* cdesc, int32_t* zero_word, hipStream_t s,
+                                    int64_t* qbase = nullptr, int runs = 0) {
   FIA_HIP_TRY(scan_state(c, Q, s));
   FIA_HIP_TRY(c->flag.reserve(64, s));
   const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
   unsigned int* ctr = reinterpret_cast<unsigned int*>(c->qscan.as<char>() + c->qscan.bytes - 16);
   hipLaunchKernelGGL(k_query_scan<MODE>, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, qu, qi, Q,
                      c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I, out,
-                     c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word);
+                     c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word, qbase, runs);
   return hipGetLastError();
 }
 
@@ -574,12 +631,22 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
   return hipGetLastError();
 }
 
+// queries per item-run block (A/B knob FIA_RUN_QB, 1 = no sharing)
+static int run_qb() {
+  static const int v = getenv("FIA_RUN_QB") ? atoi(getenv("FIA_RUN_QB")) : 4;
+  return v < 1 ? 1 : v > kRunQB ? kRunQB : v;
+}
+
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word) {
+                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word, bool runs) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1), s));
-  if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
+  if (!offsets_only) {
+    FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
+    FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1), s));
+  }
   return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
-                              offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s);
+                              offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s,
+                              offsets_only ? nullptr : c->qbase.as<int64_t>(), (runs && !offsets_only) ? run_qb() : 0);
 }
 
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,

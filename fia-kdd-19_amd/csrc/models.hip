@@ -824,6 +824,13 @@ struct GramSides {
   const double* lgm[2];
   const float* W3;
   int64_t N;
+  // MF residual pass (k_gram_mf_mfma): e_p = r-hat_p - y_p per list position -> lres[side][N]
+  const float* emb_self[2];
+  const float* bias_self[2];
+  const float* bias_other[2];
+  const float* rating[2];
+  const float* gbias;
+  double* lres;
 };
 
 
@@ -924,6 +931,64 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
     if (grp == 0 && 16 * t + col < K) out[tri(K, 16 * t + col)] = s;
   }
   if (lane == 0) out[tri(K, K)] = (double)len;
+}
+
+// MF residual per list position of each side, over the Gram work items (a wave per
+// item, a position per lane; the other-side rows come from L2, the Gram pass just
+// gathered them): e_p = theta_e . g_p + (b_e + g) + b_o - y, summed in the order the
+// per-(rating, query) scoring dots used -> lres[side][N] for k_score_mf_res
+template <class M>
+__global__ __launch_bounds__(64) void k_resid_list_mf(GramSides GSd) {
+  constexpr int K = M::K;
+  const int sd = (int64_t)blockIdx.x >= GSd.n_items[0] ? 1 : 0;
+  const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
+  if (w >= GSd.n_items[sd]) return;
+  const int32_t* __restrict__ items = GSd.items[sd];
+  const int32_t e = items[4 * w], start = items[4 * w + 1], len = items[4 * w + 2];
+  const int lane = threadIdx.x;
+  const float* __restrict__ Es = GSd.emb_self[sd] + (int64_t)e * K;
+  const float* __restrict__ emb_other = GSd.emb_other[sd];
+  const double bsg = (double)GSd.bias_self[sd][e] + (double)GSd.gbias[0];
+  const float* __restrict__ bo = GSd.bias_other[sd];
+  const int64_t lb = GSd.ptr[sd][e] + start;
+  const float* __restrict__ rat = GSd.rating[sd] + lb;
+  const int32_t* __restrict__ oth = GSd.other[sd] + lb;
+  double* __restrict__ lr = GSd.lres + (int64_t)sd * GSd.N + lb;
+  // 4 positions per lane per round, every load of the round issued before the first use
+  // (a Gram item is <= 256 positions at k <= 16: one round)
+  constexpr int PR = 4;
+  for (int p0 = 0; p0 < len; p0 += 64 * PR) {
+    int32_t o[PR];
+    float y[PR], bb[PR];
+    float4 t[PR][K / 4];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      const int p = p0 + 64 * r + lane;
+      const int pc = p < len ? p : 0;
+      o[r] = oth[pc];
+      y[r] = rat[pc];
+    }
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      const float4* row = reinterpret_cast<const float4*>(emb_other + (int64_t)o[r] * K);
+#pragma unroll
+      for (int c4 = 0; c4 < K / 4; ++c4) t[r][c4] = row[c4];
+      bb[r] = bo[o[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      double dot = 0.0;
+#pragma unroll
+      for (int c4 = 0; c4 < K / 4; ++c4) {
+        dot = fma((double)Es[4 * c4 + 0], (double)t[r][c4].x, dot);
+        dot = fma((double)Es[4 * c4 + 1], (double)t[r][c4].y, dot);
+        dot = fma((double)Es[4 * c4 + 2], (double)t[r][c4].z, dot);
+        dot = fma((double)Es[4 * c4 + 3], (double)t[r][c4].w, dot);
+      }
+      const int p = p0 + 64 * r + lane;
+      if (p < len) lr[p] = dot + bsg + (double)bb[r] - (double)y[r];
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1194,6 +1259,282 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
 // chunk's descriptor, list entries and record words are loaded while the current
 // chunk's gathers are in flight, so each chunk waits on one round trip.
 // ------------------------------------------------------------------------------------
+// k_score_mf_run (MF k <= 16, the headline kernel): the per-query chunks of k_score_mf,
+// except that an item-side chunk is scored ONCE for a run of consecutive batch queries
+// with the same test item (<= kRunQB, runs cut at multiples of kRunQB): the run's first
+// query ("head") gathers the chunk's other-side rows once and scores every query of the
+// run; the other queries' item-side descriptors are skipped.  A batch in item-major
+// order (the usual way to answer a test set) shares each popular item's list this way
+// without any group build; any order stays correct (runs of one).  Random 64-B row
+// gathers from the L2-resident tables are what bound the per-query kernel (tools/
+// mb_score.hip: 54 us without them vs 105 us with them at ml-1m-ex), so they are cut
+// to one per (rating, run).  Per chunk: e_j from the Gram pass's residual (A.lres), the
+// run's per-query words (x, 1/n, c_q, x_bias, the dup other, output / slot bases) by one
+// vector load round trip, lane (a, j) holding coordinates 4a..4a+3 of query j, then
+// broadcast per query by v_readlane as SGPR operands.
+//   influence_jq = (2 e_j (x_q . g_j + x_bias,q) + c_q) / n_q          (mf:237-246)
+
+template <class M>
+__global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
+    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
+    const int64_t* __restrict__ qbase, const double* __restrict__ rec, int64_t* __restrict__ rel_idx,
+    double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(!M::ncf && M::K <= 16 && M::K % 4 == 0, "MF k in {8, 16}");
+  constexpr int K = M::K, NA = K / 4, SPC = kScoreRows;
+  const int lane = threadIdx.x & 63, jl = lane & 15, al = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t ntask = qbase[4 * Q] * SPC;      // (work descriptor, quarter) tasks
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  for (int64_t tk = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; tk < ntask; tk += stride) {
+    const ChunkDesc d = cdesc[tk / SPC];
+    const int qt = (int)(tk % SPC);
+    const int sd = d.side & 0xff, nq = d.side >> 8;
+    const int32_t q = d.q;
+    const int32_t qj = q + (jl < nq ? jl : nq - 1);
+    const int idx = 64 * qt + lane;              // position in the chunk of this lane's rating
+    const bool ok = idx < d.len;
+    // list entry of the lane's rating (past the chunk's end: its first entry)
+    int32_t o, row;
+    double e;
+    {
+      const int li = ok ? idx : 0;
+      o = A.other[sd][d.list_base + li];
+      row = A.row[sd][d.list_base + li];
+      e = A.lres[(int64_t)sd * A.N + d.list_base + li];
+    }
+    // the run's per-query words: lane (a, j) = query q + j (clamped), coordinates 4a..4a+3
+    double xa[4];
+    double inv_n, cq, xsb;
+    int32_t dupo;
+    int64_t obj, cbj, pbj;
+    {
+      const double* __restrict__ Rj = rec + (int64_t)qj * M::R;
+      const double* __restrict__ Sj = Rj + 4 + sd * M::SB;
+      const int a = al < NA ? al : NA - 1;
+      const double2* xs = reinterpret_cast<const double2*>(Sj + K + 4 * a);
+      const double2 x01 = xs[0], x23 = xs[1];
+      xa[0] = x01.x; xa[1] = x01.y; xa[2] = x23.x; xa[3] = x23.y;
+      inv_n = Rj[0];
+      cq = Rj[1];
+      xsb = Sj[2 * K + 1];
+      dupo = (int32_t)Sj[2 * K + 2];
+      const longlong2* qb = reinterpret_cast<const longlong2*>(qbase + 4 * (int64_t)qj);
+      const longlong2 q01 = qb[0], q23 = qb[1];
+      obj = sd ? q01.y : q01.x;
+      cbj = sd ? q23.y : q23.x;
+      pbj = sd ? q01.y - q01.x : 0;
+    }
+    float g[K];
+    {
+      const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
+      const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o * K);
+#pragma unroll
+      for (int c = 0; c < NA; ++c) {
+        const float4 t = src[c];
+        g[4 * c] = t.x; g[4 * c + 1] = t.y; g[4 * c + 2] = t.z; g[4 * c + 3] = t.w;
+      }
+    }
+    const int64_t ob0 = ((int64_t)__builtin_amdgcn_readlane((int)(obj >> 32), 0) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(obj & 0xffffffff), 0);
+    const int64_t co = d.out_base - ob0;     // chunk offset inside the side segment (x kChunk)
+    // every load the query loop reads is consumed here: at the loop header hipcc cannot
+    // tell a pending load from the loop's own stores and would wait vmcnt(0) -- for the
+    // previous query's stores -- on every iteration
+    asm volatile("" ::"v"(o), "v"(row), "v"(e));
+#pragma unroll
+    for (int c = 0; c < K; ++c) asm volatile("" ::"v"(g[c]));
+    asm volatile("" ::"v"(xa[0]), "v"(xa[1]), "v"(xa[2]), "v"(xa[3]), "v"(inv_n), "v"(cq), "v"(xsb), "v"(dupo));
+    asm volatile("" ::"v"(obj), "v"(cbj), "v"(pbj));
+    for (int j = 0; j < nq; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int c4 = 0; c4 < NA; ++c4)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) s = fma(readlane_d(xa[cc], 16 * c4 + j), (double)g[4 * c4 + cc], s);
+      const double inv_nj = readlane_d(inv_n, j), cqj = readlane_d(cq, j), xsbj = readlane_d(xsb, j);
+      const int32_t dupj = __builtin_amdgcn_readlane(dupo, j);
+      const int64_t ob = ((int64_t)__builtin_amdgcn_readlane((int)(obj >> 32), j) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(obj & 0xffffffff), j);
+      const int64_t cb = ((int64_t)__builtin_amdgcn_readlane((int)(cbj >> 32), j) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(cbj & 0xffffffff), j);
+      const int32_t pb = __builtin_amdgcn_readlane((int)pbj, j);
+      double infl = (2.0 * e * (s + xsbj) + cqj) * inv_nj;
+      const bool dup = ok && o == dupj;
+      if (__builtin_expect(__ballot(dup) != 0, 0)) {
+        // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
+        const double* __restrict__ R = rec + (int64_t)(q + j) * M::R;
+        const double xv = R[2], rhat_ui = R[3];
+        if (dup) infl = (2.0 * (rhat_ui - (double)A.rating[sd][d.list_base + idx]) * xv + cqj) * inv_nj;
+      }
+      if (ok) {
+        if (influence) __builtin_nontemporal_store(infl, influence + ob + co + idx);
+        if (rel_idx) __builtin_nontemporal_store((int64_t)row, rel_idx + ob + co + idx);
+      }
+      if (K_top > 0) {
+        // this quarter's candidate slot set of the query's chunk
+        const int64_t slot = ((cb + co / kChunk) * SPC + qt) * K_top;
+        const double ca = ok ? topk_key(infl) : -2.0;
+        const int cp = ok ? (int)(pb + co) + idx : -1;
+        double pa = INFINITY;
+        int pp = -1;
+        for (int t = 0; t < K_top; ++t) {
+          double ba = -2.0, bv = 0.0;
+          int bp = 0x7fffffff;
+          if (cp >= 0 && better(pa, pp, ca, cp)) { ba = ca; bp = cp; bv = infl; }
+          wave_best(ba, bp, bv);
+          if (lane == 0) {
+            const bool okk = ba > -1.5;
+            cand_pos[slot + t] = okk ? bp : -1;
+            cand_val[slot + t] = okk ? bv : NAN;
+          }
+          pa = ba;
+          pp = bp;
+        }
+      }
+    }
+  }
+}
+
+// k_score_mf_res: the same chunks and outputs with e_j read from the residual the Gram
+// pass stored per list position (A.lres, coalesced 8 B) instead of a per-(rating, query)
+// dot with the entity's embedding, and the chunk's x / header taken from the record by
+// scalar loads as SGPR operands (no readlane broadcasts, no SGPR spills).  Per rating
+// and query what is left is s_j = x . g_j: k converts + k FMAs on the gathered row.
+template <class M>
+__global__ __launch_bounds__(kScoreThreads) void k_score_mf_res(
+    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
+    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(!M::ncf, "MF scoring");
+  constexpr int K = M::K, RT = kScoreRows;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nchunks = coff[Q];
+  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
+  const int64_t N = A.N;
+  struct Stage {
+    int32_t o[RT], row[RT];
+    double e[RT];
+  };
+  // list entries of chunk d (positions past its end clamped to its first entry)
+  auto fetch = [&](const ChunkDesc& d, Stage& st) {
+    const int sd = d.side;
+    const int32_t* __restrict__ oth = A.other[sd] + d.list_base;
+    const int32_t* __restrict__ rw = A.row[sd] + d.list_base;
+    const double* __restrict__ res = A.lres + (int64_t)sd * N + d.list_base;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int idx = r * 64 + lane;
+      const int li = idx < d.len ? idx : 0;
+      st.o[r] = oth[li];
+      st.row[r] = rw[li];
+      st.e[r] = res[li];
+    }
+  };
+  int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave;
+  if (ch >= nchunks) return;
+  ChunkDesc d = cdesc[ch];
+  Stage cur;
+  fetch(d, cur);
+  while (true) {
+    const int sd = d.side;
+    float4 g4[RT][K / 4];
+    {
+      const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)cur.o[r] * K);
+#pragma unroll
+        for (int c = 0; c < K / 4; ++c) g4[r][c] = src[c];
+      }
+    }
+    // the next chunk's descriptor and list entries behind the gathers (unconditional:
+    // past the last chunk the current one is fetched again and not used)
+    const int64_t nx = ch + stride;
+    const ChunkDesc dn = cdesc[nx < nchunks ? nx : ch];
+    Stage nxt;
+    fetch(dn, nxt);
+    const double* __restrict__ R = rec + (int64_t)d.q * M::R;
+    const double* __restrict__ Sg = R + 4 + sd * M::SB;
+    double s[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) s[r] = 0.0;
+#pragma unroll
+    for (int c4 = 0; c4 < K / 4; ++c4) {
+      double gd[RT][4];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        gd[r][0] = g4[r][c4].x; gd[r][1] = g4[r][c4].y; gd[r][2] = g4[r][c4].z; gd[r][3] = g4[r][c4].w;
+      }
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const double xc = Sg[K + 4 * c4 + cc];        // scalar load, SGPR operand
+#pragma unroll
+        for (int r = 0; r < RT; ++r) s[r] = fma(xc, gd[r][cc], s[r]);
+      }
+    }
+    const double inv_n = R[0], cq = R[1];
+    const double xsb = Sg[2 * K + 1];
+    const int32_t dupo = (int32_t)Sg[2 * K + 2];
+    double infl[RT];
+    bool dup[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      dup[r] = cur.o[r] == dupo && r * 64 + lane < d.len;
+      infl[r] = (2.0 * cur.e[r] * (s[r] + xsb) + cq) * inv_n;
+    }
+    bool anyd = false;
+#pragma unroll
+    for (int r = 0; r < RT; ++r) anyd = anyd || dup[r];
+    if (__builtin_expect(__ballot(anyd) != 0, 0)) {
+      // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
+      const double xv = R[2], rhat_ui = R[3];
+      const float* __restrict__ rat = A.rating[sd] + d.list_base;
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+        if (dup[r]) infl[r] = (2.0 * (rhat_ui - (double)rat[r * 64 + lane]) * xv + cq) * inv_n;
+    }
+    double ca[RT];
+    int cp[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int idx = r * 64 + lane;
+      const bool ok = idx < d.len;
+      if (ok) {
+        if (influence) __builtin_nontemporal_store(infl[r], influence + d.out_base + idx);
+        if (rel_idx) __builtin_nontemporal_store((int64_t)cur.row[r], rel_idx + d.out_base + idx);
+      }
+      cp[r] = ok ? d.pos0 + idx : -1;
+      ca[r] = ok ? topk_key(infl[r]) : -2.0;
+    }
+    if (K_top > 0) {
+      double pa = INFINITY;
+      int pp = -1;
+      for (int t = 0; t < K_top; ++t) {
+        double ba = -2.0, bv = 0.0;
+        int bp = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
+            ba = ca[r]; bp = cp[r]; bv = infl[r];
+          }
+        wave_best(ba, bp, bv);
+        if (lane == 0) {
+          const bool okk = ba > -1.5;
+          cand_pos[ch * K_top + t] = okk ? bp : -1;
+          cand_val[ch * K_top + t] = okk ? bv : NAN;
+        }
+        pa = ba;
+        pp = bp;
+      }
+    }
+    if (nx >= nchunks) break;
+    ch = nx;
+    d = dn;
+    cur = nxt;
+  }
+}
+
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_mf(
     QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
@@ -2286,6 +2627,12 @@ constexpr bool use_tps() {
   return !M::ncf && M::Ds <= 17;
 }
 
+// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): run | res | old
+static const char* mf_score_mode() {
+  static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "old";
+  return m;
+}
+
 template <class M>
 hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   constexpr int Ds = M::Ds, GS = Ds * (Ds + 1) / 2, K = M::K;
@@ -2315,7 +2662,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   const Index& X = c->idx;
   for (int sd = 0; sd < 2; ++sd)
     if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP), s));
-  GramSides G;
+  GramSides G{};
   for (int sd = 0; sd < 2; ++sd) {
     G.n_items[sd] = n_ent[sd] > 0 ? X.n_gitems[sd] : 0;
     G.items[sd] = X.gitems[sd].as<int32_t>();
@@ -2345,9 +2692,25 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
       FIA_HIP_TRY(hipGetLastError());
     }
   } else {
+    // e_p per list position of each side, for the scoring kernels
+    FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * X.N + 1), s));
+    for (int sd = 0; sd < 2; ++sd) {
+      G.emb_self[sd] = c->p.t[sd];
+      G.bias_self[sd] = c->p.t[2 + sd];
+      G.bias_other[sd] = c->p.t[3 - sd];
+      G.rating[sd] = X.side[sd].rating.as<float>();
+    }
+    G.gbias = c->p.t[4];
+    G.lres = c->resid.as<double>();
     if (G.n_items[0] + G.n_items[1] > 0) {
       hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
       FIA_HIP_TRY(hipGetLastError());
+      // per-list-position residuals: only the FIA_MF_SCORE=res scoring variant reads them
+      const bool res_mode = strcmp(mf_score_mode(), "old") != 0;
+      if (res_mode && M::K <= 16) {
+        hipLaunchKernelGGL(k_resid_list_mf<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
+        FIA_HIP_TRY(hipGetLastError());
+      }
     }
   }
   const int64_t nc0 = n_ent[0] > 0 ? X.n_gcomb[0] : 0, nc1 = n_ent[1] > 0 ? X.n_gcomb[1] : 0;
@@ -2381,7 +2744,11 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int qblock = use_mfma ? kMfmaQB : query_block<M>();
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
-  const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
+  // MF k <= 16 per-query chunks: k_score_mf_run (A/B knob FIA_MF_SCORE=run|res|old), one
+  // candidate slot set per 64-rating quarter of a chunk
+  const char* mfs = mf_score_mode();
+  const bool runs = !M::ncf && M::K <= 16 && !grouped && !strcmp(mfs, "run");
+  const int spc = runs ? kScoreRows : grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   if (K > 0) {
     FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc), s));
@@ -2395,7 +2762,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // solve and finished full-D; the chunk scan zeroes the count
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
-  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>()));
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? cpi_used : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
@@ -2421,10 +2788,11 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
-  int64_t grid = (max_items + 3) / 4;            // 4 waves (work items) per block
+  int64_t grid = runs ? max_items : (max_items + 3) / 4;   // 4 waves (work items / quarters) per block
   if (grid < 1) grid = 1;
   // grid cap (measured): NCF 1024 workgroups (yelp-ex score 0.314 -> 0.290 ms), MF 8192
-  constexpr int64_t gcap = M::ncf ? 1024 : 8192;
+  static const int64_t genv = getenv("FIA_SCORE_GRID") ? atoll(getenv("FIA_SCORE_GRID")) : 0;  // A/B knob
+  const int64_t gcap = genv > 0 ? genv : M::ncf ? 1024 : 8192;
   if (grid > gcap) grid = gcap;
   phase_begin(c, 2, s);
   if (grouped) {
@@ -2458,13 +2826,28 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
                          c->cand_val.as<double>());
   } else {
-    if constexpr (!M::ncf)
-      hipLaunchKernelGGL(k_score_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q,
-                         c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(), c->rec.as<double>(), rel_idx, influence,
-                         K, c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+    // A/B knob FIA_MF_SCORE: run (default, k <= 16) | res | old (per-query residual dots)
+    if constexpr (!M::ncf) {
+      if constexpr (M::K <= 16) {
+        if (runs) {
+          hipLaunchKernelGGL(k_score_mf_run<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q,
+                             c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
+                             c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
+                             c->cand_val.as<double>());
+          FIA_HIP_TRY(hipGetLastError());
+          phase_end(c, 2, s);
+          goto topk;
+        }
+      }
+      hipLaunchKernelGGL(strcmp(mfs, "old") ? k_score_mf_res<M> : k_score_mf<M>, dim3((unsigned)grid),
+                         dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(),
+                         c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
+                         c->cand_val.as<double>());
+    }
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);
+topk:
   if (K > 0 && Q > 0) {
     phase_begin(c, 3, s);
     FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, spc, topk_pos, topk_idx, topk_val, s, max_chunks));
