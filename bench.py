@@ -137,7 +137,8 @@ def score_kernel(cfg, K=1):
     if model == "NCF":
         return "k_score_ncf"
     if k <= 16:
-        return "k_score_mf" if os.environ.get("FIA_MF_SCORE_OLD") else "k_score_mf_res"
+        mode = os.environ.get("FIA_MF_SCORE", "old")
+        return {"run": "k_score_mf_run", "res": "k_score_mf_res"}.get(mode, "k_score_mf")
     if k in (32, 64) and K <= 1 and not os.environ.get("FIA_NO_MFMA_SCORE"):
         return "k_score_mf_mfma"
     return "k_score_grouped_mf"

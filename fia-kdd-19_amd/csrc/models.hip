@@ -834,6 +834,68 @@ struct GramSides {
 };
 
 
+// MF residual per list position of a Gram work item's slice (k_resid_list_mf: a wave per
+// item right after the Gram pass, so the other-side rows come from L2):
+// e_p = theta_e . g_p + (b_e + g) + b_o - y, summed in the order the per-(rating, query)
+// scoring dots used -> lres[side][N] for k_score_mf_run
+template <class M>
+__device__ __forceinline__ void resid_slice(const GramSides& GSd, int sd, int32_t e, int32_t start, int32_t len,
+                                            int lane) {
+  constexpr int K = M::K;
+  const float* __restrict__ Es = GSd.emb_self[sd] + (int64_t)e * K;
+  const float* __restrict__ emb_other = GSd.emb_other[sd];
+  const double bsg = (double)GSd.bias_self[sd][e] + (double)GSd.gbias[0];
+  const float* __restrict__ bo = GSd.bias_other[sd];
+  const int64_t lb = GSd.ptr[sd][e] + start;
+  const float* __restrict__ rat = GSd.rating[sd] + lb;
+  const int32_t* __restrict__ oth = GSd.other[sd] + lb;
+  double* __restrict__ lr = GSd.lres + (int64_t)sd * GSd.N + lb;
+  // 4 positions per lane per round, every load of the round issued before the first use
+  // (a Gram item is <= 256 positions at k <= 16: one round)
+  constexpr int PR = 4;
+  for (int p0 = 0; p0 < len; p0 += 64 * PR) {
+    int32_t o[PR];
+    float y[PR], bb[PR];
+    float4 t[PR][K / 4];
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      const int p = p0 + 64 * r + lane;
+      const int pc = p < len ? p : 0;
+      o[r] = oth[pc];
+      y[r] = rat[pc];
+    }
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      const float4* row = reinterpret_cast<const float4*>(emb_other + (int64_t)o[r] * K);
+#pragma unroll
+      for (int c4 = 0; c4 < K / 4; ++c4) t[r][c4] = row[c4];
+      bb[r] = bo[o[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      double dot = 0.0;
+#pragma unroll
+      for (int c4 = 0; c4 < K / 4; ++c4) {
+        dot = fma((double)Es[4 * c4 + 0], (double)t[r][c4].x, dot);
+        dot = fma((double)Es[4 * c4 + 1], (double)t[r][c4].y, dot);
+        dot = fma((double)Es[4 * c4 + 2], (double)t[r][c4].z, dot);
+        dot = fma((double)Es[4 * c4 + 3], (double)t[r][c4].w, dot);
+      }
+      const int p = p0 + 64 * r + lane;
+      if (p < len) lr[p] = dot + bsg + (double)bb[r] - (double)y[r];
+    }
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(64) void k_resid_list_mf(GramSides GSd) {
+  const int sd = (int64_t)blockIdx.x >= GSd.n_items[0] ? 1 : 0;
+  const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
+  if (w >= GSd.n_items[sd]) return;
+  const int32_t* __restrict__ items = GSd.items[sd];
+  resid_slice<M>(GSd, sd, items[4 * w], items[4 * w + 1], items[4 * w + 2], threadIdx.x);
+}
+
 template <class M>
 __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
   constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
@@ -931,64 +993,6 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
     if (grp == 0 && 16 * t + col < K) out[tri(K, 16 * t + col)] = s;
   }
   if (lane == 0) out[tri(K, K)] = (double)len;
-}
-
-// MF residual per list position of each side, over the Gram work items (a wave per
-// item, a position per lane; the other-side rows come from L2, the Gram pass just
-// gathered them): e_p = theta_e . g_p + (b_e + g) + b_o - y, summed in the order the
-// per-(rating, query) scoring dots used -> lres[side][N] for k_score_mf_res
-template <class M>
-__global__ __launch_bounds__(64) void k_resid_list_mf(GramSides GSd) {
-  constexpr int K = M::K;
-  const int sd = (int64_t)blockIdx.x >= GSd.n_items[0] ? 1 : 0;
-  const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
-  if (w >= GSd.n_items[sd]) return;
-  const int32_t* __restrict__ items = GSd.items[sd];
-  const int32_t e = items[4 * w], start = items[4 * w + 1], len = items[4 * w + 2];
-  const int lane = threadIdx.x;
-  const float* __restrict__ Es = GSd.emb_self[sd] + (int64_t)e * K;
-  const float* __restrict__ emb_other = GSd.emb_other[sd];
-  const double bsg = (double)GSd.bias_self[sd][e] + (double)GSd.gbias[0];
-  const float* __restrict__ bo = GSd.bias_other[sd];
-  const int64_t lb = GSd.ptr[sd][e] + start;
-  const float* __restrict__ rat = GSd.rating[sd] + lb;
-  const int32_t* __restrict__ oth = GSd.other[sd] + lb;
-  double* __restrict__ lr = GSd.lres + (int64_t)sd * GSd.N + lb;
-  // 4 positions per lane per round, every load of the round issued before the first use
-  // (a Gram item is <= 256 positions at k <= 16: one round)
-  constexpr int PR = 4;
-  for (int p0 = 0; p0 < len; p0 += 64 * PR) {
-    int32_t o[PR];
-    float y[PR], bb[PR];
-    float4 t[PR][K / 4];
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      const int p = p0 + 64 * r + lane;
-      const int pc = p < len ? p : 0;
-      o[r] = oth[pc];
-      y[r] = rat[pc];
-    }
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      const float4* row = reinterpret_cast<const float4*>(emb_other + (int64_t)o[r] * K);
-#pragma unroll
-      for (int c4 = 0; c4 < K / 4; ++c4) t[r][c4] = row[c4];
-      bb[r] = bo[o[r]];
-    }
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      double dot = 0.0;
-#pragma unroll
-      for (int c4 = 0; c4 < K / 4; ++c4) {
-        dot = fma((double)Es[4 * c4 + 0], (double)t[r][c4].x, dot);
-        dot = fma((double)Es[4 * c4 + 1], (double)t[r][c4].y, dot);
-        dot = fma((double)Es[4 * c4 + 2], (double)t[r][c4].z, dot);
-        dot = fma((double)Es[4 * c4 + 3], (double)t[r][c4].w, dot);
-      }
-      const int p = p0 + 64 * r + lane;
-      if (p < len) lr[p] = dot + bsg + (double)bb[r] - (double)y[r];
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1280,27 +1284,31 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
     const int64_t* __restrict__ qbase, const double* __restrict__ rec, int64_t* __restrict__ rel_idx,
     double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && M::K <= 16 && M::K % 4 == 0, "MF k in {8, 16}");
-  constexpr int K = M::K, NA = K / 4, SPC = kScoreRows;
+  constexpr int K = M::K, RT = kScoreRows, NA = K / 4;
   const int lane = threadIdx.x & 63, jl = lane & 15, al = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t ntask = qbase[4 * Q] * SPC;      // (work descriptor, quarter) tasks
+  const int64_t nwork = qbase[4 * Q];            // compacted work descriptors (build_chunks runs)
   const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  for (int64_t tk = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; tk < ntask; tk += stride) {
-    const ChunkDesc d = cdesc[tk / SPC];
-    const int qt = (int)(tk % SPC);
+  for (int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; ch < nwork; ch += stride) {
+    const ChunkDesc d = cdesc[ch];
     const int sd = d.side & 0xff, nq = d.side >> 8;
     const int32_t q = d.q;
     const int32_t qj = q + (jl < nq ? jl : nq - 1);
-    const int idx = 64 * qt + lane;              // position in the chunk of this lane's rating
-    const bool ok = idx < d.len;
-    // list entry of the lane's rating (past the chunk's end: its first entry)
-    int32_t o, row;
-    double e;
+    // list entries of the chunk (positions past its end clamped to its first entry)
+    int32_t o[RT], row[RT];
+    double e[RT];
     {
-      const int li = ok ? idx : 0;
-      o = A.other[sd][d.list_base + li];
-      row = A.row[sd][d.list_base + li];
-      e = A.lres[(int64_t)sd * A.N + d.list_base + li];
+      const int32_t* __restrict__ oth = A.other[sd] + d.list_base;
+      const int32_t* __restrict__ rw = A.row[sd] + d.list_base;
+      const double* __restrict__ res = A.lres + (int64_t)sd * A.N + d.list_base;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int idx = r * 64 + lane;
+        const int li = idx < d.len ? idx : 0;
+        o[r] = oth[li];
+        row[r] = rw[li];
+        e[r] = res[li];
+      }
     }
     // the run's per-query words: lane (a, j) = query q + j (clamped), coordinates 4a..4a+3
     double xa[4];
@@ -1324,14 +1332,17 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
       cbj = sd ? q23.y : q23.x;
       pbj = sd ? q01.y - q01.x : 0;
     }
-    float g[K];
+    float g[RT][K];
     {
       const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
-      const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o * K);
 #pragma unroll
-      for (int c = 0; c < NA; ++c) {
-        const float4 t = src[c];
-        g[4 * c] = t.x; g[4 * c + 1] = t.y; g[4 * c + 2] = t.z; g[4 * c + 3] = t.w;
+      for (int r = 0; r < RT; ++r) {
+        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o[r] * K);
+#pragma unroll
+        for (int c = 0; c < NA; ++c) {
+          const float4 t = src[c];
+          g[r][4 * c] = t.x; g[r][4 * c + 1] = t.y; g[r][4 * c + 2] = t.z; g[r][4 * c + 3] = t.w;
+        }
       }
     }
     const int64_t ob0 = ((int64_t)__builtin_amdgcn_readlane((int)(obj >> 32), 0) << 32) |
@@ -1340,17 +1351,33 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
     // every load the query loop reads is consumed here: at the loop header hipcc cannot
     // tell a pending load from the loop's own stores and would wait vmcnt(0) -- for the
     // previous query's stores -- on every iteration
-    asm volatile("" ::"v"(o), "v"(row), "v"(e));
 #pragma unroll
-    for (int c = 0; c < K; ++c) asm volatile("" ::"v"(g[c]));
+    for (int r = 0; r < RT; ++r) {
+      asm volatile("" ::"v"(o[r]), "v"(row[r]), "v"(e[r]));
+#pragma unroll
+      for (int c = 0; c < K; ++c) asm volatile("" ::"v"(g[r][c]));
+    }
     asm volatile("" ::"v"(xa[0]), "v"(xa[1]), "v"(xa[2]), "v"(xa[3]), "v"(inv_n), "v"(cq), "v"(xsb), "v"(dupo));
     asm volatile("" ::"v"(obj), "v"(cbj), "v"(pbj));
     for (int j = 0; j < nq; ++j) {
-      double s = 0.0;
+      double s[RT];
+      {
 #pragma unroll
-      for (int c4 = 0; c4 < NA; ++c4)
+        for (int r = 0; r < RT; ++r) s[r] = 0.0;
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) s = fma(readlane_d(xa[cc], 16 * c4 + j), (double)g[4 * c4 + cc], s);
+        for (int c4 = 0; c4 < NA; ++c4) {
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            asm volatile("" : "+v"(g[r][4 * c4]), "+v"(g[r][4 * c4 + 1]), "+v"(g[r][4 * c4 + 2]),
+                         "+v"(g[r][4 * c4 + 3]), "+v"(s[r]));
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            const double xc = readlane_d(xa[cc], 16 * c4 + j);
+#pragma unroll
+            for (int r = 0; r < RT; ++r) s[r] = fma(xc, (double)g[r][4 * c4 + cc], s[r]);
+          }
+        }
+      }
       const double inv_nj = readlane_d(inv_n, j), cqj = readlane_d(cq, j), xsbj = readlane_d(xsb, j);
       const int32_t dupj = __builtin_amdgcn_readlane(dupo, j);
       const int64_t ob = ((int64_t)__builtin_amdgcn_readlane((int)(obj >> 32), j) << 32) |
@@ -1358,180 +1385,81 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
       const int64_t cb = ((int64_t)__builtin_amdgcn_readlane((int)(cbj >> 32), j) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)(cbj & 0xffffffff), j);
       const int32_t pb = __builtin_amdgcn_readlane((int)pbj, j);
-      double infl = (2.0 * e * (s + xsbj) + cqj) * inv_nj;
-      const bool dup = ok && o == dupj;
-      if (__builtin_expect(__ballot(dup) != 0, 0)) {
+      double infl[RT];
+      bool dup[RT];
+      bool anyd = false;
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        dup[r] = o[r] == dupj && r * 64 + lane < d.len;
+        anyd = anyd || dup[r];
+        infl[r] = (2.0 * e[r] * (s[r] + xsbj) + cqj) * inv_nj;
+      }
+      if (__builtin_expect(__ballot(anyd) != 0, 0)) {
         // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
         const double* __restrict__ R = rec + (int64_t)(q + j) * M::R;
         const double xv = R[2], rhat_ui = R[3];
-        if (dup) infl = (2.0 * (rhat_ui - (double)A.rating[sd][d.list_base + idx]) * xv + cqj) * inv_nj;
+        const float* __restrict__ rat = A.rating[sd] + d.list_base;
+#pragma unroll
+        for (int r = 0; r < RT; ++r)
+          if (dup[r]) infl[r] = (2.0 * (rhat_ui - (double)rat[r * 64 + lane]) * xv + cqj) * inv_nj;
       }
-      if (ok) {
-        if (influence) __builtin_nontemporal_store(infl, influence + ob + co + idx);
-        if (rel_idx) __builtin_nontemporal_store((int64_t)row, rel_idx + ob + co + idx);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx < d.len) {
+          if (influence) __builtin_nontemporal_store(infl[r], influence + ob + co + idx);
+          if (rel_idx) __builtin_nontemporal_store((int64_t)row[r], rel_idx + ob + co + idx);
+        }
       }
-      if (K_top > 0) {
-        // this quarter's candidate slot set of the query's chunk
-        const int64_t slot = ((cb + co / kChunk) * SPC + qt) * K_top;
-        const double ca = ok ? topk_key(infl) : -2.0;
-        const int cp = ok ? (int)(pb + co) + idx : -1;
+      if (K_top == 1) {
+        // running best over the lane's rows (positions ascend with r), then over the wave
+        double ba = -2.0, bv = 0.0;
+        int bp = 0x7fffffff;
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const int idx = r * 64 + lane;
+          const double key = idx < d.len ? topk_key(infl[r]) : -2.0;
+          if (key > ba) { ba = key; bp = (int)(pb + co) + idx; bv = infl[r]; }
+        }
+        wave_best(ba, bp, bv);
+        if (lane == 0) {
+          const int64_t slot = cb + co / kChunk;
+          const bool okk = ba > -1.5;
+          cand_pos[slot] = okk ? bp : -1;
+          cand_val[slot] = okk ? bv : NAN;
+        }
+      } else if (K_top > 1) {
+        double ca[RT];
+        int cp[RT];
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const int idx = r * 64 + lane;
+          const bool ok = idx < d.len;
+          cp[r] = ok ? (int)(pb + co) + idx : -1;
+          ca[r] = ok ? topk_key(infl[r]) : -2.0;
+        }
+        const int64_t slot = cb + co / kChunk;
         double pa = INFINITY;
         int pp = -1;
         for (int t = 0; t < K_top; ++t) {
           double ba = -2.0, bv = 0.0;
           int bp = 0x7fffffff;
-          if (cp >= 0 && better(pa, pp, ca, cp)) { ba = ca; bp = cp; bv = infl; }
+#pragma unroll
+          for (int r = 0; r < RT; ++r)
+            if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
+              ba = ca[r]; bp = cp[r]; bv = infl[r];
+            }
           wave_best(ba, bp, bv);
           if (lane == 0) {
             const bool okk = ba > -1.5;
-            cand_pos[slot + t] = okk ? bp : -1;
-            cand_val[slot + t] = okk ? bv : NAN;
+            cand_pos[slot * K_top + t] = okk ? bp : -1;
+            cand_val[slot * K_top + t] = okk ? bv : NAN;
           }
           pa = ba;
           pp = bp;
         }
       }
     }
-  }
-}
-
-// k_score_mf_res: the same chunks and outputs with e_j read from the residual the Gram
-// pass stored per list position (A.lres, coalesced 8 B) instead of a per-(rating, query)
-// dot with the entity's embedding, and the chunk's x / header taken from the record by
-// scalar loads as SGPR operands (no readlane broadcasts, no SGPR spills).  Per rating
-// and query what is left is s_j = x . g_j: k converts + k FMAs on the gathered row.
-template <class M>
-__global__ __launch_bounds__(kScoreThreads) void k_score_mf_res(
-    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
-    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf, "MF scoring");
-  constexpr int K = M::K, RT = kScoreRows;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nchunks = coff[Q];
-  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  const int64_t N = A.N;
-  struct Stage {
-    int32_t o[RT], row[RT];
-    double e[RT];
-  };
-  // list entries of chunk d (positions past its end clamped to its first entry)
-  auto fetch = [&](const ChunkDesc& d, Stage& st) {
-    const int sd = d.side;
-    const int32_t* __restrict__ oth = A.other[sd] + d.list_base;
-    const int32_t* __restrict__ rw = A.row[sd] + d.list_base;
-    const double* __restrict__ res = A.lres + (int64_t)sd * N + d.list_base;
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int idx = r * 64 + lane;
-      const int li = idx < d.len ? idx : 0;
-      st.o[r] = oth[li];
-      st.row[r] = rw[li];
-      st.e[r] = res[li];
-    }
-  };
-  int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave;
-  if (ch >= nchunks) return;
-  ChunkDesc d = cdesc[ch];
-  Stage cur;
-  fetch(d, cur);
-  while (true) {
-    const int sd = d.side;
-    float4 g4[RT][K / 4];
-    {
-      const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)cur.o[r] * K);
-#pragma unroll
-        for (int c = 0; c < K / 4; ++c) g4[r][c] = src[c];
-      }
-    }
-    // the next chunk's descriptor and list entries behind the gathers (unconditional:
-    // past the last chunk the current one is fetched again and not used)
-    const int64_t nx = ch + stride;
-    const ChunkDesc dn = cdesc[nx < nchunks ? nx : ch];
-    Stage nxt;
-    fetch(dn, nxt);
-    const double* __restrict__ R = rec + (int64_t)d.q * M::R;
-    const double* __restrict__ Sg = R + 4 + sd * M::SB;
-    double s[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) s[r] = 0.0;
-#pragma unroll
-    for (int c4 = 0; c4 < K / 4; ++c4) {
-      double gd[RT][4];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        gd[r][0] = g4[r][c4].x; gd[r][1] = g4[r][c4].y; gd[r][2] = g4[r][c4].z; gd[r][3] = g4[r][c4].w;
-      }
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const double xc = Sg[K + 4 * c4 + cc];        // scalar load, SGPR operand
-#pragma unroll
-        for (int r = 0; r < RT; ++r) s[r] = fma(xc, gd[r][cc], s[r]);
-      }
-    }
-    const double inv_n = R[0], cq = R[1];
-    const double xsb = Sg[2 * K + 1];
-    const int32_t dupo = (int32_t)Sg[2 * K + 2];
-    double infl[RT];
-    bool dup[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      dup[r] = cur.o[r] == dupo && r * 64 + lane < d.len;
-      infl[r] = (2.0 * cur.e[r] * (s[r] + xsb) + cq) * inv_n;
-    }
-    bool anyd = false;
-#pragma unroll
-    for (int r = 0; r < RT; ++r) anyd = anyd || dup[r];
-    if (__builtin_expect(__ballot(anyd) != 0, 0)) {
-      // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
-      const double xv = R[2], rhat_ui = R[3];
-      const float* __restrict__ rat = A.rating[sd] + d.list_base;
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-        if (dup[r]) infl[r] = (2.0 * (rhat_ui - (double)rat[r * 64 + lane]) * xv + cq) * inv_n;
-    }
-    double ca[RT];
-    int cp[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int idx = r * 64 + lane;
-      const bool ok = idx < d.len;
-      if (ok) {
-        if (influence) __builtin_nontemporal_store(infl[r], influence + d.out_base + idx);
-        if (rel_idx) __builtin_nontemporal_store((int64_t)cur.row[r], rel_idx + d.out_base + idx);
-      }
-      cp[r] = ok ? d.pos0 + idx : -1;
-      ca[r] = ok ? topk_key(infl[r]) : -2.0;
-    }
-    if (K_top > 0) {
-      double pa = INFINITY;
-      int pp = -1;
-      for (int t = 0; t < K_top; ++t) {
-        double ba = -2.0, bv = 0.0;
-        int bp = 0x7fffffff;
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
-            ba = ca[r]; bp = cp[r]; bv = infl[r];
-          }
-        wave_best(ba, bp, bv);
-        if (lane == 0) {
-          const bool okk = ba > -1.5;
-          cand_pos[ch * K_top + t] = okk ? bp : -1;
-          cand_val[ch * K_top + t] = okk ? bv : NAN;
-        }
-        pa = ba;
-        pp = bp;
-      }
-    }
-    if (nx >= nchunks) break;
-    ch = nx;
-    d = dn;
-    cur = nxt;
   }
 }
 
@@ -2627,7 +2555,7 @@ constexpr bool use_tps() {
   return !M::ncf && M::Ds <= 17;
 }
 
-// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): run | res | old
+// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): run | old
 static const char* mf_score_mode() {
   static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "old";
   return m;
@@ -2701,16 +2629,18 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
       G.rating[sd] = X.side[sd].rating.as<float>();
     }
     G.gbias = c->p.t[4];
-    G.lres = c->resid.as<double>();
+    // per-list-position residuals (fused into the Gram pass): read by k_score_mf_run only
+    G.lres = (M::K <= 16 && !strcmp(mf_score_mode(), "run")) ? c->resid.as<double>() : nullptr;
     if (G.n_items[0] + G.n_items[1] > 0) {
       hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
       FIA_HIP_TRY(hipGetLastError());
-      // per-list-position residuals: only the FIA_MF_SCORE=res scoring variant reads them
-      const bool res_mode = strcmp(mf_score_mode(), "old") != 0;
-      if (res_mode && M::K <= 16) {
+      // the residual pass as its own launch over the same work items (fused into the Gram
+      // wave it raised that kernel's VGPRs 64 -> 128: ml-1m-ex prepare 78 -> 88 us)
+      if (G.lres) {
         hipLaunchKernelGGL(k_resid_list_mf<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
-        FIA_HIP_TRY(hipGetLastError());
       }
+      FIA_HIP_TRY(hipGetLastError());
+
     }
   }
   const int64_t nc0 = n_ent[0] > 0 ? X.n_gcomb[0] : 0, nc1 = n_ent[1] > 0 ? X.n_gcomb[1] : 0;
@@ -2745,10 +2675,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
   // MF k <= 16 per-query chunks: k_score_mf_run (A/B knob FIA_MF_SCORE=run|res|old), one
-  // candidate slot set per 64-rating quarter of a chunk
+  // candidate slot set per chunk
   const char* mfs = mf_score_mode();
   const bool runs = !M::ncf && M::K <= 16 && !grouped && !strcmp(mfs, "run");
-  const int spc = runs ? kScoreRows : grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
+  const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   if (K > 0) {
     FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc), s));
@@ -2788,7 +2718,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
-  int64_t grid = runs ? max_items : (max_items + 3) / 4;   // 4 waves (work items / quarters) per block
+  int64_t grid = (max_items + 3) / 4;            // 4 waves (work items) per block
   if (grid < 1) grid = 1;
   // grid cap (measured): NCF 1024 workgroups (yelp-ex score 0.314 -> 0.290 ms), MF 8192
   static const int64_t genv = getenv("FIA_SCORE_GRID") ? atoll(getenv("FIA_SCORE_GRID")) : 0;  // A/B knob
@@ -2839,7 +2769,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
           goto topk;
         }
       }
-      hipLaunchKernelGGL(strcmp(mfs, "old") ? k_score_mf_res<M> : k_score_mf<M>, dim3((unsigned)grid),
+      hipLaunchKernelGGL(k_score_mf<M>, dim3((unsigned)grid),
                          dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(),
                          c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
                          c->cand_val.as<double>());

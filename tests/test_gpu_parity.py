@@ -396,3 +396,22 @@ def test_mf_entity_shared_topk_paths(k, K, tmp_path):
         assert rel_err(res["influence"][b:e], o["influence"]) < RTOL, (k, K, q)
         assert np.array_equal(res["topk_pos"][q][:min(K, e - b)], fo.topk(res["influence"][b:e], K)), (k, K, q)
         check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], K)
+
+
+def test_mf_item_run_schedule_variant():
+    """The opt-in MF k <= 16 item-run schedule (FIA_MF_SCORE=run: k_score_mf_run + the
+    per-list-position residual pass) passes the same MF golden, duplicate-row, full-ml-1m-ex
+    and scan-window checks.  The schedule is read once per process, so the checks run in a
+    child pytest with the knob set."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FIA_MF_SCORE="run", FIA_RUN_QB="4")
+    sel = ("small_golden and mf or duplicate_rows or ml1m_rq1_golden and MF or ml1m_all_queries "
+           "or ml1m_deterministic or many_queries_scan_windows and MF-16 or every_built_size and MF-8 "
+           "or every_built_size and MF-16")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.join(root, "tests", "test_gpu_parity.py"), "-m", "gpu",
+                        "-q", "-x", "-p", "no:cacheprovider", "-k", sel], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and "deselected" in r.stdout
