@@ -640,13 +640,12 @@ static int run_qb() {
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word, bool runs) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1), s));
-  if (!offsets_only) {
-    FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
-    FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1), s));
-  }
+  const bool rq = runs && !offsets_only;
+  if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
+  if (rq) FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1), s));
   return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
                               offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s,
-                              offsets_only ? nullptr : c->qbase.as<int64_t>(), (runs && !offsets_only) ? run_qb() : 0);
+                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? run_qb() : 0);
 }
 
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
