@@ -145,12 +145,13 @@ def score_kernel(cfg, K=1):
 
 
 def bytes_per_query(model, k, n):
-    """SURVEY.md 8d algorithmic bytes per query: MF n(4k+32) + 8k+8; NCF n(8k+32).  Counts the
-    gathered rows once per query (the entity-shared kernels load them once per query block)."""
+    """SURVEY.md 8d algorithmic bytes per query, with the train-row output as int32 (4 B, not
+    the survey's 8 B): MF n(4k+28) + 8k+8; NCF n(8k+28).  Counts the gathered rows once per
+    query (the entity-shared kernels load them once per query block)."""
     n = np.asarray(n, np.float64)
     if model == "MF":
-        return n * (4 * k + 32) + 8 * k + 8
-    return n * (8 * k + 32)
+        return n * (4 * k + 28) + 8 * k + 8
+    return n * (8 * k + 28)
 
 
 _CPU = {}     # state the forked CPU-baseline workers inherit
@@ -421,7 +422,7 @@ def main():
         batches.append((b0, b1, qb_u, qb_i, off_b, tot_b))
     max_rows = max([b[5] for b in batches] + [1])
     max_q = max([b[1] - b[0] for b in batches] + [1])
-    rel = torch.empty(max_rows, dtype=torch.int64, device=dev)
+    rel = torch.empty(max_rows, dtype=torch.int32, device=dev)
     infl = torch.empty(max_rows, dtype=torch.float64, device=dev)
     xbuf = torch.empty(max_q * D, dtype=torch.float64, device=dev)
     tp = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev)

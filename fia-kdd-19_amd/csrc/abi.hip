@@ -266,7 +266,7 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
 }
 
 int fia_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                int64_t* rel_idx, void* stream) {
+                int32_t* rel_idx, void* stream) {
   if (!c) return FIA_ERR_INVALID;
   FIA_GUARDED(c, {
     if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
@@ -280,7 +280,7 @@ int fia_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, con
 }
 
 int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                    int64_t total_rel, int64_t* rel_idx, double* influence, double* x_out, int K,
+                    int64_t total_rel, int32_t* rel_idx, double* influence, double* x_out, int K,
                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream) {
   if (!c) return FIA_ERR_INVALID;
   FIA_GUARDED(c, {

@@ -1269,7 +1269,7 @@ template <class M>
 __global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
     BigArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   constexpr int K = M::K, SW = score_waves<M>(), QB = kBigQueryBlock, RSW = 4 + M::SB;
   constexpr int NPASS = kScoreRows;
@@ -1369,7 +1369,7 @@ __global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
         const int64_t obj = bl[j];
         if (ok) {
           if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-          if (rel_idx) __builtin_nontemporal_store((int64_t)row, rel_idx + obj + idx);
+          if (rel_idx) __builtin_nontemporal_store(row, rel_idx + obj + idx);
         }
         if (K_top > 0) {
           const int64_t cbj = bl[QB + j];
@@ -1419,7 +1419,7 @@ template <class M>
 __global__ __launch_bounds__(256) void k_big_score_mfma(
     BigArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   constexpr int K = M::K, KD = score_kd<M>(), QB = kBigMfmaQB, XS = QB + 1, NPASS = kScoreRows;
   static_assert(NPASS == 4, "one wave per scoring pass");
@@ -1555,7 +1555,7 @@ __global__ __launch_bounds__(256) void k_big_score_mfma(
         const int idx = 64 * wave + 16 * t + ml;
         if (ok[t] && j < nq) {
           if (influence) influence[obj + idx] = infl;
-          if (rel_idx) rel_idx[obj + idx] = (int64_t)rw[t];
+          if (rel_idx) rel_idx[obj + idx] = rw[t];
         }
         acc[t][r] = infl;
         la[r][t] = ok[t] ? topk_key(infl) : -2.0;
@@ -1830,7 +1830,7 @@ hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, c
 
 template <class M>
 hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                          int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                          int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                           int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
   constexpr int NPs = M::NPs, NPASS = kScoreRows, SW = score_waves<M>();
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
@@ -1929,7 +1929,7 @@ hipError_t check_cover(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
 }
 
 hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                     int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                     int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
 #define X(m, kk, T)                                                                                            \
   if (c->p.model == m && c->p.k == kk)                                                                         \

@@ -206,7 +206,7 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
 hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
                          int64_t* offsets, hipStream_t s);
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
-                         const int64_t* offsets, int64_t* rel, hipStream_t s);
+                         const int64_t* offsets, int32_t* rel, hipStream_t s);
 // per-query chunk offsets coff (+ chunk descriptors unless offsets_only; with `runs` the
 // descriptors are the compacted work list of k_score_mf_run: every user-side chunk, the
 // item-side chunks of run heads only, their count at qbase[4Q])
@@ -222,7 +222,7 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported);
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                       int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                       int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                        int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
                        bool& unsupported);
 int model_num_params(int model, int k);
@@ -236,7 +236,7 @@ hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
 // flag[2] |= 1 if a query's user or item has no cache after fia_prepare_for
 hipError_t check_cover(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag, hipStream_t s);
 hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                     int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                     int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,

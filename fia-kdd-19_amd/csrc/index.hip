@@ -424,7 +424,7 @@ __global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned l
 __global__ void k_write_related(const int32_t* __restrict__ qu, const int32_t* __restrict__ qi,
                                 const int64_t* __restrict__ offsets, const int64_t* __restrict__ uptr,
                                 const int32_t* __restrict__ urow, const int64_t* __restrict__ iptr,
-                                const int32_t* __restrict__ irow, int64_t U, int64_t I, int64_t* __restrict__ rel) {
+                                const int32_t* __restrict__ irow, int64_t U, int64_t I, int32_t* __restrict__ rel) {
   int64_t q = blockIdx.x;
   int32_t u = qu[q], i = qi[q];
   if (u < 0 || u >= U || i < 0 || i >= I) return;
@@ -623,7 +623,7 @@ hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 }
 
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                         int64_t* rel, hipStream_t s) {
+                         int32_t* rel, hipStream_t s) {
   if (Q == 0) return hipSuccess;
   hipLaunchKernelGGL(k_write_related, dim3((unsigned)Q), dim3(256), 0, s, qu, qi, offsets,
                      c->idx.side[0].ptr.as<int64_t>(), c->idx.side[0].row.as<int32_t>(),

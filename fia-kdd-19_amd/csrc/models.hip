@@ -1281,7 +1281,7 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
     QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
-    const int64_t* __restrict__ qbase, const double* __restrict__ rec, int64_t* __restrict__ rel_idx,
+    const int64_t* __restrict__ qbase, const double* __restrict__ rec, int32_t* __restrict__ rel_idx,
     double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && M::K <= 16 && M::K % 4 == 0, "MF k in {8, 16}");
   constexpr int K = M::K, RT = kScoreRows, NA = K / 4;
@@ -1408,7 +1408,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
         const int idx = r * 64 + lane;
         if (idx < d.len) {
           if (influence) __builtin_nontemporal_store(infl[r], influence + ob + co + idx);
-          if (rel_idx) __builtin_nontemporal_store((int64_t)row[r], rel_idx + ob + co + idx);
+          if (rel_idx) __builtin_nontemporal_store(row[r], rel_idx + ob + co + idx);
         }
       }
       if (K_top == 1) {
@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
 template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_mf(
     QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf, "MF scoring");
   constexpr int K = M::K, RT = kScoreRows, NV = (M::SB + 63) / 64;
@@ -1565,7 +1565,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf(
       const double infl = (2.0 * e * s + cq) * inv_n;
       if (ok) {
         if (influence) __builtin_nontemporal_store(infl, influence + d.out_base + idx);
-        if (rel_idx) __builtin_nontemporal_store((int64_t)cur.row[r], rel_idx + d.out_base + idx);
+        if (rel_idx) __builtin_nontemporal_store(cur.row[r], rel_idx + d.out_base + idx);
       }
       cp[r] = ok ? d.pos0 + idx : -1;
       ca[r] = ok ? topk_key(infl) : -2.0;
@@ -1617,7 +1617,7 @@ template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf, "MF scoring (NCF: k_score_ncf)");
   constexpr int K = M::K;
@@ -1765,7 +1765,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
           const int idx = (h * RW + r) * 64 + lane;
           if (ok_[r]) {   // streaming outputs: nontemporal, so they do not evict the gathered tables from L2
             if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-            if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+            if (rel_idx) __builtin_nontemporal_store(row_[r], rel_idx + obj + idx);
           }
           lp[r] = ok_[r] ? cidx * kChunk + idx : -1;    // related position inside this side's list
           la[r] = ok_[r] ? topk_key(infl) : -2.0;
@@ -1823,7 +1823,7 @@ template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && M::K % 4 == 0, "MF, k a multiple of 4");
   constexpr int K = M::K, RT = kScoreRows, QB = query_block<M>(), CK = 4;
@@ -1945,7 +1945,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
           const int idx = r * 64 + lane;
           if (ok_[r]) {
             if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-            if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+            if (rel_idx) __builtin_nontemporal_store(row_[r], rel_idx + obj + idx);
           }
           lp[r] = ok_[r] ? cidx * kChunk + idx : -1;
           la[r] = ok_[r] ? topk_key(infl) : -2.0;
@@ -2028,7 +2028,7 @@ template <class M, bool FULL, int CPI, int SETUP>
 __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
   constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, TPC = kChunk / 16;
@@ -2097,7 +2097,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     // per D row r (query m = kk + 4 r): influence = fma(e * al, D + xb, be) at outp[r][p]
     double al[4], be[4], xb[4];
     double* outp[4];
-    int64_t* relp[4];
+    int32_t* relp[4];
     int32_t dupo[4], cpos[4];
     int64_t cslot[4];
     bool qv[4];
@@ -2232,7 +2232,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
           const double* __restrict__ R = rec + (int64_t)q * M::R;
           const double infl = fma((R[3] - y) * al[r], R[2], be[r]);
           if (FULL || influence) st_out(infl, outp[r] + 16 * t);
-          if (FULL || rel_idx) st_out((int64_t)w, relp[r] + 16 * t);
+          if (FULL || rel_idx) st_out(w, relp[r] + 16 * t);
           const long long key = topk_ikey(infl);
           if (key > bk[r]) { bk[r] = key; bp[r] = p; bv[r] = infl; }
         }
@@ -2243,7 +2243,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
         const double infl = fma(en * al[r], acc[r] + xb[r], be[r]);
         if (ok) {
           if (FULL || influence) st_out(infl, outp[r] + 16 * t);
-          if (FULL || rel_idx) st_out((int64_t)w, relp[r] + 16 * t);
+          if (FULL || rel_idx) st_out(w, relp[r] + 16 * t);
         }
         const long long key = ok ? topk_ikey(infl) : -2ll;
         const bool take = key > bk[r];
@@ -2285,7 +2285,7 @@ template <class M>
 __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int64_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
+    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(M::ncf && M::K % 4 == 0, "NCF, k a multiple of 4");
   constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4;
@@ -2392,7 +2392,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
           const int idx = r * 64 + lane;
           if (ok_[r]) {
             if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-            if (rel_idx) __builtin_nontemporal_store((int64_t)row_[r], rel_idx + obj + idx);
+            if (rel_idx) __builtin_nontemporal_store(row_[r], rel_idx + obj + idx);
           }
           lp[r] = ok_[r] ? cidx * kChunk + idx : -1;
           la[r] = ok_[r] ? topk_key(infl) : -2.0;
@@ -2655,7 +2655,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
 
 template <class M>
 hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                      int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                      int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
   // Auto schedule (measured on MI355X, profiles/): entity-shared scoring wins whenever
   // the per-rating work is larger than a 64-B gather (k >= 32) -- 20M MF k=64 855 vs
@@ -2838,7 +2838,7 @@ hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported) {
 }
 
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                       int64_t max_chunks, int64_t* rel_idx, double* influence, double* x_out, int K,
+                       int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                        int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s, bool& unsupported) {
   unsupported = false;
 #define X(m, kk, T)                                                                                        \

@@ -145,12 +145,21 @@ class Context(object):
         self._check(rc, "fia_count_related")
         return offsets, (total.value if want_total else None)
 
+    @staticmethod
+    def _need_int32(t, name):
+        # the library writes train rows as int32 (include/fia.h fia_related)
+        import torch
+        if t is not None and t.dtype != torch.int32:
+            raise TypeError("%s must be a torch.int32 tensor (got %s)" % (name, t.dtype))
+
     def related(self, qu, qi, offsets, rel_idx):
+        self._need_int32(rel_idx, "rel_idx")
         rc = self.lib.fia_related(self.h, qu.numel(), _ptr(qu), _ptr(qi), _ptr(offsets), _ptr(rel_idx), _stream())
         self._check(rc, "fia_related")
 
     def query_batch(self, qu, qi, offsets, total, rel_idx=None, influence=None, x=None, K=0,
                     topk_pos=None, topk_idx=None, topk_val=None):
+        self._need_int32(rel_idx, "rel_idx")
         rc = self.lib.fia_query_batch(self.h, qu.numel(), _ptr(qu), _ptr(qi), _ptr(offsets), int(total),
                                       _ptr(rel_idx), _ptr(influence), _ptr(x), int(K), _ptr(topk_pos),
                                       _ptr(topk_idx), _ptr(topk_val), _stream())

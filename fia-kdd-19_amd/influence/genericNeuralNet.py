@@ -332,9 +332,9 @@ class GenericNeuralNet(object):
         self.test_u, self.test_i = self._test_pair(test_indices[0])
         qu, qi = self._query_tensors(test_indices)
         offsets, total = self.ctx.count_related(qu, qi)
-        rel = torch.empty(max(total, 1), dtype=torch.int64, device=self.ctx.torch_device)
+        rel = torch.empty(max(total, 1), dtype=torch.int32, device=self.ctx.torch_device)
         self.ctx.related(qu, qi, offsets, rel)
-        return rel[:total].cpu().numpy()
+        return rel[:total].cpu().numpy().astype(np.int64)     # the reference's np.where dtype
 
     def get_test_params(self, test_index):
         """theta_t values in the reference block order (mf:38-67 / ncf:43-66)."""
@@ -352,7 +352,7 @@ class GenericNeuralNet(object):
         dev = self.ctx.torch_device
         offsets, total = self.ctx.count_related(qu, qi)
         D = self.ctx.num_params()
-        rel = torch.empty(max(total, 1), dtype=torch.int64, device=dev) if full else None
+        rel = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if full else None
         infl = torch.empty(max(total, 1), dtype=torch.float64, device=dev) if full else None
         x = torch.empty(max(Q * D, 1), dtype=torch.float64, device=dev) if return_x else None
         tp = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev) if K else None
@@ -361,7 +361,7 @@ class GenericNeuralNet(object):
         self.ctx.query_batch(qu, qi, offsets, total, rel, infl, x, K, tp, ti, tv)
         out = dict(offsets=offsets.cpu().numpy())
         if full:
-            out["rel_idx"] = rel[:total].cpu().numpy()
+            out["rel_idx"] = rel[:total].cpu().numpy().astype(np.int64)
             out["influence"] = infl[:total].cpu().numpy()
         if return_x:
             out["x"] = x[:Q * D].cpu().numpy().reshape(Q, D)

@@ -109,14 +109,17 @@ int fia_prepare_for(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, co
 int fia_count_related(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const int32_t* q_item,
                       int64_t* offsets, int64_t* total_out, void* stream);
 
-/* rel_idx[offsets[q] + p] = p-th train row of the related list of query q. */
+/* rel_idx[offsets[q] + p] = p-th train row of the related list of query q (device
+ * int32: fia_build_index limits n_train to < 2^31, so every train row fits; the reference's
+ * np.where gives int64 -- the Python facade widens on the copy to the host, and the
+ * device writes 4 B instead of 8 B per related rating). */
 int fia_related(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const int32_t* q_item,
-                const int64_t* offsets, int64_t* rel_idx, void* stream);
+                const int64_t* offsets, int32_t* rel_idx, void* stream);
 
 /* Batched FIA: for every query q = (q_user[q], q_item[q]):
  *   H_t x = v solved exactly (fp64 LDL^T), then for every related rating p:
  *   influence[offsets[q]+p] = x . grad L_p / n_q   (mf:237-246),
- *   rel_idx[offsets[q]+p]   = its train row.
+ *   rel_idx[offsets[q]+p]   = its train row (int32, see fia_related).
  * x_out (nullable): device double[Q * D] in the reference theta order
  *   (MF [p_u, q_i, b_u, b_i], D = 2k+2; NCF [Pm_u, Qm_i, Pg_u, Qg_i], D = 4k).
  * rel_idx / influence may be NULL to skip writing the full vectors.
@@ -128,7 +131,7 @@ int fia_related(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const 
  * and a NaN x (TF's mean over an empty batch). */
 int fia_query_batch(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const int32_t* q_item,
                     const int64_t* offsets, int64_t total_rel,
-                    int64_t* rel_idx, double* influence, double* x_out,
+                    int32_t* rel_idx, double* influence, double* x_out,
                     int K, int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream);
 
 /* Number of restricted parameters D of the registered model (0 if none). */

@@ -105,7 +105,7 @@ def run_batches(ctx, qu_np, qi_np, K, checker, keep=()):
         bounds.append(min(n_q.size, max(b1, b0 + 1)))
     max_rows = int(max(cum[b1] - cum[b0] for b0, b1 in zip(bounds[:-1], bounds[1:])))
     D = ctx.num_params()
-    rel = torch.empty(max_rows, dtype=torch.int64, device=dev)
+    rel = torch.empty(max_rows, dtype=torch.int32, device=dev)
     infl = torch.empty(max_rows, dtype=torch.float64, device=dev)
     out = {}
     total = 0

@@ -60,7 +60,7 @@ def _answer(model, k, U, I, train, qu_np, qi_np, tables_np, K):
         ctx.prepare()
     offs, tot = ctx.count_related(qu, qi)
     Q = qu.numel()
-    rel = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+    rel = torch.empty(max(tot, 1), dtype=torch.int32, device=dev)
     infl = torch.empty(max(tot, 1), dtype=torch.float64, device=dev)
     tp = torch.empty(Q * K, dtype=torch.int64, device=dev)
     tix = torch.empty_like(tp)
