@@ -1463,8 +1463,12 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
   }
 }
 
+// waves per SIMD the headline kernel is compiled for (A/B: -DFIA_SCORE_WAVES=5 spills 68 B/lane)
+#ifndef FIA_SCORE_WAVES
+#define FIA_SCORE_WAVES 4
+#endif
 template <class M>
-__global__ __launch_bounds__(kScoreThreads) void k_score_mf(
+__global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(FIA_SCORE_WAVES))) void k_score_mf(
     QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
     const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
