@@ -123,6 +123,23 @@ struct PairTable {
       h = (h + 1) & mask;
     }
   }
+  // the same lookup split in two: the first probe's load is issued early, the rest of the
+  // chain (rarely more than one probe at load <= 1/2) resolves later
+  __device__ inline void probe_start(unsigned long long k, unsigned long long& h, unsigned long long& kk) const {
+    h = pair_hash(k) & mask;
+    kk = key[h];
+  }
+  __device__ inline void probe_finish(unsigned long long k, unsigned long long h, unsigned long long kk, double& c,
+                                      double& s) const {
+    c = 0.0;
+    s = 0.0;
+    for (unsigned long long probe = 0; probe <= mask; ++probe) {
+      if (kk == k) { c = (double)cnt[h]; s = sum[h]; return; }
+      if (kk == kEmptyKey) return;
+      h = (h + 1) & mask;
+      kk = key[h];
+    }
+  }
 };
 
 // Parameter table pointers (device, float32, owned by the caller).

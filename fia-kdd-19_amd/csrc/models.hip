@@ -63,6 +63,9 @@ struct NCFm {
 
 __device__ __forceinline__ int tri(int r, int c) { return (r * (r + 1)) / 2 + c; }
 
+// 4 doubles per lane: an f64 MFMA 16x16 tile (C/D layout: element (4 r + (l >> 4), l & 15) in [r])
+typedef double d4_t __attribute__((ext_vector_type(4)));
+
 // lane l's double, broadcast to the wave (v_readlane into SGPRs; l compile-time)
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const long long b = __double_as_longlong(v);
@@ -434,6 +437,145 @@ struct QueryArgs {
   int64_t N;
 };
 
+// theta_t, v = d r(u,i)/d theta_t (gnn:155, mf:194,201 / ncf:222,229) and r-hat(u,i) of one
+// query into the workgroup's LDS arrays th[D] / g[D] (NTH threads cooperate; r-hat is
+// valid in the first wave)
+template <class M, int NTH>
+__device__ double solve_prologue(const QueryArgs& A, int32_t u, int32_t i, double* __restrict__ th,
+                                 double* __restrict__ g, double* __restrict__ sh, const NCFWeights<M::ncf ? M::K : 2>& w,
+                                 const double* __restrict__ sW1, const double* __restrict__ sb1) {
+  constexpr int K = M::K, Ds = M::Ds;
+  const int lane = threadIdx.x;
+  double rhat_ui = 0.0;
+  if constexpr (!M::ncf) {
+    const float* P = A.t[0];
+    const float* Qt = A.t[1];
+    for (int a = lane; a < K; a += NTH) {
+      th[a] = P[(int64_t)u * K + a];
+      th[Ds + a] = Qt[(int64_t)i * K + a];
+      g[a] = Qt[(int64_t)i * K + a];           // user block of v: q_i
+      g[Ds + a] = P[(int64_t)u * K + a];       // item block of v: p_u
+    }
+    if (lane == 0) {
+      th[K] = A.t[2][u];
+      th[Ds + K] = A.t[3][i];
+      g[K] = 1.0;
+      g[Ds + K] = 1.0;
+    }
+    __syncthreads();
+    double part = 0.0;
+    for (int a = lane; a < K; a += NTH) part += th[a] * th[Ds + a];
+    rhat_ui = wave_sum(part) + th[K] + th[Ds + K] + (double)A.t[4][0];
+  } else {
+    constexpr int H2 = K / 2;
+    const float* Pm = A.t[0];
+    const float* Qm = A.t[1];
+    const float* Pg = A.t[2];
+    const float* Qg = A.t[3];
+    double* z1 = sh;            // K
+    double* d2 = sh + K;        // K/2
+    double* d1 = sh + 2 * K;    // K
+    for (int a = lane; a < K; a += NTH) {
+      th[a] = Pm[(int64_t)u * K + a];
+      th[K + a] = Pg[(int64_t)u * K + a];
+      th[Ds + a] = Qm[(int64_t)i * K + a];
+      th[Ds + K + a] = Qg[(int64_t)i * K + a];
+      z1[a] = A.l1[0][(int64_t)u * K + a] + A.l1[1][(int64_t)i * K + a] + sb1[a];
+    }
+    __syncthreads();
+    double mlp_part = 0.0;
+    for (int dd2 = lane; dd2 < H2; dd2 += NTH) {
+      double z2 = w.b2[dd2];
+      for (int c = 0; c < K; ++c) z2 = fma(w.W2[c * H2 + dd2], z1[c] > 0.0 ? z1[c] : 0.0, z2);
+      const bool on = z2 > 0.0;
+      d2[dd2] = on ? w.W3[dd2] : 0.0;
+      mlp_part += on ? w.W3[dd2] * z2 : 0.0;
+    }
+    double gmf_part = 0.0;
+    for (int a = lane; a < K; a += NTH) gmf_part += w.W3[H2 + a] * th[K + a] * th[Ds + K + a];
+    rhat_ui = wave_sum(mlp_part + gmf_part) + (double)A.t[9][0];
+    __syncthreads();
+    for (int c = lane; c < K; c += NTH) {
+      double t = 0.0;
+      for (int dd2 = 0; dd2 < H2; ++dd2) t = fma(w.W2[c * H2 + dd2], d2[dd2], t);
+      d1[c] = z1[c] > 0.0 ? t : 0.0;
+    }
+    __syncthreads();
+    for (int a = lane; a < 2 * K; a += NTH) {
+      // rows a < K: W1[:k] (Pm part, user block); rows a >= K: W1[k:] (Qm part, item block)
+      double s = 0.0;
+      for (int c = 0; c < K; ++c) s = fma(sW1[a * K + c], d1[c], s);
+      if (a < K) g[a] = s; else g[Ds + (a - K)] = s;
+    }
+    for (int a = lane; a < K; a += NTH) {
+      g[K + a] = w.W3[H2 + a] * th[Ds + K + a];        // d r/d Pg_u = W3g * Qg_i
+      g[Ds + K + a] = w.W3[H2 + a] * th[K + a];        // d r/d Qg_i = W3g * Pg_u
+    }
+  }
+  __syncthreads();
+  return rhat_ui;
+}
+
+// Record + x_out of one solved query (first wave only, 64 lanes): v = the solution in
+// block order [user block (Ds) | item block (Ds)]
+template <class M>
+__device__ void solve_epilogue(const QueryArgs& A, int64_t q, int32_t u, int32_t i, int64_t n, double rhat_ui,
+                               const double* __restrict__ th, const double* __restrict__ g,
+                               const double* __restrict__ v, const NCFWeights<M::ncf ? M::K : 2>& w,
+                               double* __restrict__ R, double* __restrict__ x_out) {
+  constexpr int K = M::K, Ds = M::Ds, D = M::D;
+  const int lane = threadIdx.x & 63;
+  if (x_out)
+    for (int a = lane; a < D; a += kSolveThreads) x_out[q * D + M::ref_index(a)] = v[a];
+  double cq = 0.0, xg_user = 0.0, xg_item = 0.0;
+  for (int a = lane; a < D; a += kSolveThreads) {
+    const int j = a < Ds ? a : a - Ds;
+    if (M::decayed(j)) cq += v[a] * th[a];
+    if (a < Ds) xg_user += v[a] * g[a]; else xg_item += v[a] * g[a];
+  }
+  cq = wave_sum(cq) * A.wd;
+  xg_user = wave_sum(xg_user);
+  xg_item = wave_sum(xg_item);
+  // The (u,i) train row itself has g = v, so x.g = x.v and e = r-hat(u,i) - y: both of
+  // its copies in rel (user side and item side) get bit-identical influence, as the
+  // reference's per-row sess.run gives them (mf:240-246).
+  if (lane == 0) {
+    R[0] = 1.0 / (double)n;
+    R[1] = cq;
+    R[2] = xg_user + xg_item;
+    R[3] = rhat_ui;
+  }
+  double* S0 = R + 4;
+  double* S1 = R + 4 + M::SB;
+  if constexpr (!M::ncf) {
+    const double gb = (double)A.t[4][0];
+    for (int a = lane; a < K; a += kSolveThreads) {
+      S0[a] = th[a];              // p_u
+      S0[K + a] = v[a];           // x_pu
+      S1[a] = th[Ds + a];         // q_i
+      S1[K + a] = v[Ds + a];      // x_qi
+    }
+    if (lane == 0) {
+      S0[2 * K] = th[K] + gb;     S1[2 * K] = th[Ds + K] + gb;
+      S0[2 * K + 1] = v[K];       S1[2 * K + 1] = v[Ds + K];
+      S0[2 * K + 2] = (double)i;  S1[2 * K + 2] = (double)u;
+    }
+  } else {
+    // x . g_j = x_mlp . g_mlp,j + (W3g * x_gmf) . gmf_other(j)  (k_score_ncf)
+    constexpr int H2 = K / 2;
+    for (int c = lane; c < K; c += kSolveThreads) {
+      S0[c] = v[c];
+      S1[c] = v[Ds + c];
+      const double w3g = w.W3[H2 + c];
+      S0[K + c] = w3g * v[K + c];
+      S1[K + c] = w3g * v[Ds + K + c];
+    }
+    if (lane == 0) {
+      S0[2 * K] = (double)i;  S1[2 * K] = (double)u;
+    }
+  }
+}
+
 // One wave per query.  COLS: the two blocks of a query whose test pair is not a train row
 // are solved by ldlt_cols (the path for NCF and MF k >= 32); queries whose pair IS a train
 // row (coupled blocks) are appended to `coupled` {count, q...} for the full-D launch.
@@ -475,74 +617,7 @@ __global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(
   }
   const double s2n = 2.0 / (double)n;
 
-  // ---- theta_t and v = d r(u,i)/d theta_t (gnn:155, mf:194,201 / ncf:222,229) ----
-  double rhat_ui = 0.0;
-  if constexpr (!M::ncf) {
-    const float* P = A.t[0];
-    const float* Qt = A.t[1];
-    for (int a = lane; a < K; a += kSolveThreads) {
-      th[a] = P[(int64_t)u * K + a];
-      th[Ds + a] = Qt[(int64_t)i * K + a];
-      g[a] = Qt[(int64_t)i * K + a];           // user block of v: q_i
-      g[Ds + a] = P[(int64_t)u * K + a];       // item block of v: p_u
-    }
-    if (lane == 0) {
-      th[K] = A.t[2][u];
-      th[Ds + K] = A.t[3][i];
-      g[K] = 1.0;
-      g[Ds + K] = 1.0;
-    }
-    __syncthreads();
-    double part = 0.0;
-    for (int a = lane; a < K; a += kSolveThreads) part += th[a] * th[Ds + a];
-    rhat_ui = wave_sum(part) + th[K] + th[Ds + K] + (double)A.t[4][0];
-  } else {
-    constexpr int H2 = K / 2;
-    const float* Pm = A.t[0];
-    const float* Qm = A.t[1];
-    const float* Pg = A.t[2];
-    const float* Qg = A.t[3];
-    double* z1 = sh;            // K
-    double* d2 = sh + K;        // K/2
-    double* d1 = sh + 2 * K;    // K
-    for (int a = lane; a < K; a += kSolveThreads) {
-      th[a] = Pm[(int64_t)u * K + a];
-      th[K + a] = Pg[(int64_t)u * K + a];
-      th[Ds + a] = Qm[(int64_t)i * K + a];
-      th[Ds + K + a] = Qg[(int64_t)i * K + a];
-      z1[a] = A.l1[0][(int64_t)u * K + a] + A.l1[1][(int64_t)i * K + a] + sb1[a];
-    }
-    __syncthreads();
-    double mlp_part = 0.0;
-    for (int dd2 = lane; dd2 < H2; dd2 += kSolveThreads) {
-      double z2 = w.b2[dd2];
-      for (int c = 0; c < K; ++c) z2 = fma(w.W2[c * H2 + dd2], z1[c] > 0.0 ? z1[c] : 0.0, z2);
-      const bool on = z2 > 0.0;
-      d2[dd2] = on ? w.W3[dd2] : 0.0;
-      mlp_part += on ? w.W3[dd2] * z2 : 0.0;
-    }
-    double gmf_part = 0.0;
-    for (int a = lane; a < K; a += kSolveThreads) gmf_part += w.W3[H2 + a] * th[K + a] * th[Ds + K + a];
-    rhat_ui = wave_sum(mlp_part + gmf_part) + (double)A.t[9][0];
-    __syncthreads();
-    for (int c = lane; c < K; c += kSolveThreads) {
-      double t = 0.0;
-      for (int dd2 = 0; dd2 < H2; ++dd2) t = fma(w.W2[c * H2 + dd2], d2[dd2], t);
-      d1[c] = z1[c] > 0.0 ? t : 0.0;
-    }
-    __syncthreads();
-    for (int a = lane; a < 2 * K; a += kSolveThreads) {
-      // rows a < K: W1[:k] (Pm part, user block); rows a >= K: W1[k:] (Qm part, item block)
-      double s = 0.0;
-      for (int c = 0; c < K; ++c) s = fma(sW1[a * K + c], d1[c], s);
-      if (a < K) g[a] = s; else g[Ds + (a - K)] = s;
-    }
-    for (int a = lane; a < K; a += kSolveThreads) {
-      g[K + a] = w.W3[H2 + a] * th[Ds + K + a];        // d r/d Pg_u = W3g * Qg_i
-      g[Ds + K + a] = w.W3[H2 + a] * th[K + a];        // d r/d Qg_i = W3g * Pg_u
-    }
-  }
-  __syncthreads();
+  const double rhat_ui = solve_prologue<M, kSolveThreads>(A, u, i, th, g, sh, w, sW1, sb1);
 
   // ---- the (u,i) pair among the train rows (pair set built with the index) ----
   double cdup, rsum;
@@ -615,57 +690,453 @@ __global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(
     __syncthreads();
   }
 
-  // ---- outputs ----
-  if (x_out)
-    for (int a = lane; a < D; a += kSolveThreads) x_out[q * D + M::ref_index(a)] = v[a];
-  double cq = 0.0, xg_user = 0.0, xg_item = 0.0;
-  for (int a = lane; a < D; a += kSolveThreads) {
-    const int j = a < Ds ? a : a - Ds;
-    if (M::decayed(j)) cq += v[a] * th[a];
-    if (a < Ds) xg_user += v[a] * g[a]; else xg_item += v[a] * g[a];
-  }
-  cq = wave_sum(cq) * A.wd;
-  xg_user = wave_sum(xg_user);
-  xg_item = wave_sum(xg_item);
-  // The (u,i) train row itself has g = v, so x.g = x.v and e = r-hat(u,i) - y: both of
-  // its copies in rel (user side and item side) get bit-identical influence, as the
-  // reference's per-row sess.run gives them (mf:240-246).
-  if (lane == 0) {
-    R[0] = 1.0 / (double)n;
-    R[1] = cq;
-    R[2] = xg_user + xg_item;
-    R[3] = rhat_ui;
-  }
-  double* S0 = R + 4;
-  double* S1 = R + 4 + M::SB;
-  if constexpr (!M::ncf) {
-    const double gb = (double)A.t[4][0];
-    for (int a = lane; a < K; a += kSolveThreads) {
-      S0[a] = th[a];              // p_u
-      S0[K + a] = v[a];           // x_pu
-      S1[a] = th[Ds + a];         // q_i
-      S1[K + a] = v[Ds + a];      // x_qi
-    }
-    if (lane == 0) {
-      S0[2 * K] = th[K] + gb;     S1[2 * K] = th[Ds + K] + gb;
-      S0[2 * K + 1] = v[K];       S1[2 * K + 1] = v[Ds + K];
-      S0[2 * K + 2] = (double)i;  S1[2 * K + 2] = (double)u;
-    }
-  } else {
-    // x . g_j = x_mlp . g_mlp,j + (W3g * x_gmf) . gmf_other(j)  (k_score_ncf)
-    constexpr int H2 = K / 2;
-    for (int c = lane; c < K; c += kSolveThreads) {
-      S0[c] = v[c];
-      S1[c] = v[Ds + c];
-      const double w3g = w.W3[H2 + c];
-      S0[K + c] = w3g * v[K + c];
-      S1[K + c] = w3g * v[Ds + K + c];
-    }
-    if (lane == 0) {
-      S0[2 * K] = (double)i;  S1[2 * K] = (double)u;
-    }
-  }
+  solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, v, w, R, x_out);
   }   // work loop
+}
+
+// ------------------------------------------------------------------------------------
+// Side-system solve on 16x16 tiles (NCF, MF k >= 32): one wave per (query, side) system.
+//
+// The side block H_b (NM x NM after the MF bias is eliminated first as a Schur complement)
+// lives in registers as its upper tiles U[p][j] (p <= j) in the f64-MFMA C/D layout: lane
+// l = 16 g + c holds rows 4 r + g (r = 0..3) of column c.  In that layout a tile is at once
+// the A operand of its transpose and the B operand of itself, so the blocked right-looking
+// LDL^T needs no transposes:
+//   panel p:  the 16 rows of block p, [S | I | U[p][p+1..] | rhs_p], are eliminated by 16
+//             pivot steps (VALU; the pivot row goes through a per-wave LDS slot, the
+//             multipliers are the same row read at the lane's own rows -- S is symmetric),
+//             giving [D L^T | W = L_pp^-1 | Y_j = D Z_j | y_p]
+//   trailing: U[i][j] -= Z_i^T Y_j and rhs_i -= Z_i^T y_p on v_mfma_f64_16x16x4_f64, the
+//             right-hand side held in "column layout" (every column of its tile = the
+//             vector), so the update of the right-hand side is one more MFMA product
+//   back:     x_p = W_p^T (z_p - sum_{i>p} Z_i x_i), z_p = D^-1 y_p: a 16-lane DPP row sum
+//             and a 4-row permlane sum per block
+// Replaces the one-column-per-lane solve (LDS broadcast of every pivot column to every
+// lane: LDS-bound, and 256+256 registers with spills at MF k = 64).
+// ------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// sum over the 16 lanes of each row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror); every lane of the row gets the bit-identical sum
+__device__ __forceinline__ double row_sum16(double x) {
+  x += dpp_d<0xB1>(x);
+  x += dpp_d<0x4E>(x);
+  x += dpp_d<0x141>(x);
+  x += dpp_d<0x140>(x);
+  return x;
+}
+// sum over the 4 rows (lanes c, c+16, c+32, c+48); every lane gets the same sum
+__device__ __forceinline__ double col_sum4(double x) {
+  const long long b = __double_as_longlong(x);
+  const unsigned lo = (unsigned)(b & 0xffffffffll), hi = (unsigned)(b >> 32);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double s = __longlong_as_double(((long long)h16[0] << 32) | l16[0]) +
+                   __longlong_as_double(((long long)h16[1] << 32) | l16[1]);   // rows 0+1 | 2+3
+  const long long bs = __double_as_longlong(s);
+  const unsigned slo = (unsigned)(bs & 0xffffffffll), shi = (unsigned)(bs >> 32);
+  const auto l32 = __builtin_amdgcn_permlane32_swap(slo, slo, false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(shi, shi, false, false);
+  return __longlong_as_double(((long long)h32[0] << 32) | l32[0]) +
+         __longlong_as_double(((long long)h32[1] << 32) | l32[1]);
+}
+
+// waves per SIMD the tile solve is compiled for (registers: 4 tiles of state per 16 coordinates)
+template <class M>
+constexpr int col_waves() {
+  return M::Ds <= 16 ? 4 : 3;
+}
+
+template <class M>
+constexpr int tile_waves() {
+  return (M::ncf ? M::Ds : M::K) <= 32 ? 3 : 2;
+}
+
+__device__ __forceinline__ void pin_d4(d4_t& t) {
+  double a = t[0], b = t[1], c = t[2], d = t[3];
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+  t[0] = a; t[1] = b; t[2] = c; t[3] = d;
+}
+
+template <int NT>
+__device__ constexpr int ut(int p, int j) { return p * NT - (p * (p - 1)) / 2 + (j - p); }
+
+// Raw loads of one side system (issued together, ahead of the query's dependent prologue):
+// the upper tiles of the entity's packed lower Gram G (Ds = NM, + 1 with the MF bias), and
+// for the MF bias the bias row at the lane's rows (hr) and column (hc) and its diagonal (hb)
+template <int NT, bool EXTRA>
+__device__ __forceinline__ void tile_load(const double* __restrict__ G, int g, int c, d4_t (&U)[NT * (NT + 1) / 2],
+                                          d4_t (&hr)[NT], double (&hc)[NT], double& hb) {
+  constexpr int NM = 16 * NT;
+  const double* __restrict__ hrow = G + NM * (NM + 1) / 2;   // MF: packed row NM = the bias row
+#pragma unroll
+  for (int p = 0; p < NT; ++p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int R = 16 * p + 4 * r + g;
+#pragma unroll
+      for (int j = p; j < NT; ++j) {
+        const int C = 16 * j + c;
+        if (j > p) {
+          U[ut<NT>(p, j)][r] = G[(C * (C + 1)) / 2 + R];
+        } else {
+          const int hi = R > C ? R : C, lo = R > C ? C : R;
+          U[ut<NT>(p, j)][r] = G[(hi * (hi + 1)) / 2 + lo];
+        }
+      }
+      if constexpr (EXTRA) hr[p][r] = hrow[R];
+    }
+  if constexpr (EXTRA) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) hc[j] = hrow[16 * j + c];
+    hb = hrow[NM];
+  }
+}
+
+// One side system, from the raw loads: H = (2/n) Gram + (wd + damping) I (the MF bias, not
+// decayed, eliminated first: H - h h^T / eta, rhs - h gamma / eta), then the blocked
+// LDL^T + solves.  Rt: the right-hand side in column layout (raw, [16p + 4r + g]); gam: its
+// bias entry.  xs = the solution [Ds] (LDS, written by lanes 0..15), P = this wave's
+// pivot-row slots [2][16 * PS] (LDS).
+template <int NT, bool EXTRA>
+__device__ void tile_factor(int g, int c, d4_t (&U)[NT * (NT + 1) / 2], d4_t (&Rt)[NT], d4_t (&hr)[NT],
+                            double (&hc)[NT], double hb, double gam, double s2n, double wd, double damping,
+                            double* __restrict__ xs, double* __restrict__ P) {
+  constexpr int NM = 16 * NT, PS = (NT + 3) & ~1;
+  d4_t W[NT];
+  double ieta = 0.0;
+  if constexpr (EXTRA) {
+    ieta = 1.0 / (s2n * hb + damping);                       // the bias pivot
+#pragma unroll
+    for (int j = 0; j < NT; ++j) hc[j] *= s2n;
+  }
+#pragma unroll
+  for (int p = 0; p < NT; ++p)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int R = 16 * p + 4 * r + g;
+      const double h = EXTRA ? s2n * hr[p][r] * ieta : 0.0;
+#pragma unroll
+      for (int j = p; j < NT; ++j) {
+        double v = s2n * U[ut<NT>(p, j)][r];
+        if (j == p) v += (R == 16 * j + c) ? wd + damping : 0.0;
+        if constexpr (EXTRA) v = fma(-h, hc[j], v);
+        U[ut<NT>(p, j)][r] = v;
+      }
+      if constexpr (EXTRA) Rt[p][r] = fma(-h, gam, Rt[p][r]);
+    }
+  // ---- factor + forward solve, panel by panel ----
+#pragma unroll
+  for (int p = 0; p < NT; ++p) {
+    d4_t I;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) I[r] = (4 * r + g == c) ? 1.0 : 0.0;
+    double dv[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      double* __restrict__ Pb = P + (k & 1) * (16 * PS);
+      const int kr = k >> 2, kg = k & 3;
+      // pivot row k of the panel: slot [c][t], t = 0 S, 1 I, 2.. U[p][p+1..], last rhs
+      if (g == kg) {
+        Pb[c * PS + 0] = U[ut<NT>(p, p)][kr];
+        Pb[c * PS + 1] = I[kr];
+#pragma unroll
+        for (int j = p + 1; j < NT; ++j) Pb[c * PS + 1 + j - p] = U[ut<NT>(p, j)][kr];
+        Pb[c * PS + NT - p + 1] = Rt[p][kr];
+      }
+      wave_lds_sync();
+      const double dk = Pb[k * PS];
+      double ij = __builtin_amdgcn_rcp(dk);
+      ij = fma(ij, fma(-dk, ij, 1.0), ij);
+      ij = fma(ij, fma(-dk, ij, 1.0), ij);
+      double f[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (4 * r + 3 <= k) {
+          f[r] = 0.0;                                  // rows <= k: finished
+        } else {
+          const double m = Pb[(4 * r + g) * PS] * ij;  // S[k][row] = S[row][k]
+          f[r] = (4 * r > k || g > kg) ? m : 0.0;
+        }
+      }
+      double pv[NT + 2];
+#pragma unroll
+      for (int t = 0; t < NT - p + 2; ++t) pv[t] = Pb[c * PS + t];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (4 * r + 3 <= k) continue;
+        U[ut<NT>(p, p)][r] = fma(-f[r], pv[0], U[ut<NT>(p, p)][r]);
+        I[r] = fma(-f[r], pv[1], I[r]);
+#pragma unroll
+        for (int j = p + 1; j < NT; ++j) U[ut<NT>(p, j)][r] = fma(-f[r], pv[1 + j - p], U[ut<NT>(p, j)][r]);
+        Rt[p][r] = fma(-f[r], pv[NT - p + 1], Rt[p][r]);
+      }
+      if (g == kg) dv[kr] = ij;                        // 1/d of this lane's row k
+      // materialise this step's updates here: hipcc otherwise sinks the FMAs of rows not yet
+      // needed as pivots to their first use and keeps every step's multipliers live (spills)
+      pin_d4(U[ut<NT>(p, p)]);
+      pin_d4(I);
+#pragma unroll
+      for (int j = p + 1; j < NT; ++j) pin_d4(U[ut<NT>(p, j)]);
+      pin_d4(Rt[p]);
+      asm volatile("" : "+v"(dv[kr]));
+    }
+    W[p] = I;
+    // trailing update: U[i][j] -= Z_i^T Y_j, rhs_i -= Z_i^T y_p; keep -Z_i for the back solve
+#pragma unroll
+    for (int i = p + 1; i < NT; ++i) {
+      d4_t Zn;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Zn[r] = -U[ut<NT>(p, i)][r] * dv[r];
+#pragma unroll
+      for (int j = i; j < NT; ++j)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+          U[ut<NT>(i, j)] = __builtin_amdgcn_mfma_f64_16x16x4f64(Zn[kb], U[ut<NT>(p, j)][kb], U[ut<NT>(i, j)], 0, 0, 0);
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+        Rt[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(Zn[kb], Rt[p][kb], Rt[i], 0, 0, 0);
+      U[ut<NT>(p, i)] = Zn;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Rt[p][r] *= dv[r];     // z_p = D^-1 y_p
+  }
+  // ---- back solve: x_p = W_p^T (z_p - sum_{i>p} Z_i x_i), x in row layout (lane c) ----
+  double xr[NT];
+#pragma unroll
+  for (int p = NT - 1; p >= 0; --p) {
+    double pw = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double w = Rt[p][r];
+      if (p + 1 < NT) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = p + 1; i < NT; ++i) s = fma(U[ut<NT>(p, i)][r], xr[i], s);   // (-Z x)[4r+g]
+        w += row_sum16(s);
+      }
+      pw = fma(W[p][r], w, pw);
+    }
+    xr[p] = col_sum4(pw);
+  }
+  if constexpr (EXTRA) {                               // the bias: (gamma - h . x) / eta
+    double part = 0.0;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) part = fma(hc[j], xr[j], part);
+    part = g == 0 ? part : 0.0;
+    const double hx = wave_sum(part);
+    if ((threadIdx.x & 63) == 0) xs[NM] = (gam - hx) * ieta;
+  }
+  if (g == 0) {
+#pragma unroll
+    for (int p = 0; p < NT; ++p) xs[16 * p + c] = xr[p];
+  }
+}
+
+// Two waves per query (wave w = side w: user block, item block), persistent over queries;
+// NCF weights staged once per workgroup.  Every global load of a query (ids of the next
+// query, list pointers, the pair-set probe, both Gram blocks, MF: the right-hand side) is
+// issued before its first dependent use, so a query waits on about two memory latencies.
+// Queries whose test pair is a train row (coupled blocks) go to `coupled` {count, q...} for
+// the full-D k_solve<M, false>.
+template <class M>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(tile_waves<M>()))) void k_solve_tile(
+    QueryArgs A, int64_t Q, double* __restrict__ rec, double* __restrict__ x_out, int32_t* __restrict__ coupled_out) {
+  constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  constexpr bool EXTRA = !M::ncf;
+  constexpr int NM = EXTRA ? K : Ds, NT = NM / 16, PS = (NT + 3) & ~1, NU = NT * (NT + 1) / 2;
+  static_assert(NM % 16 == 0 && NT >= 1 && NT <= 4, "tile solve: 16..64 matrix coordinates");
+  __shared__ double th[D], g[D], xs[D];
+  __shared__ double Pv[2][2 * 16 * PS];
+  __shared__ double sh[4 * K + 8];
+  __shared__ NCFWeights<M::ncf ? K : 2> w;
+  __shared__ double sW1[M::ncf ? 2 * K * K : 1];
+  __shared__ double sb1[M::ncf ? K : 1];
+  const int wv = threadIdx.x >> 6;
+  if constexpr (M::ncf) {
+    load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
+    for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
+    for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
+  }
+  int64_t q = blockIdx.x;
+  int32_t un = q < Q ? A.qu[q] : 0, in = q < Q ? A.qi[q] : 0;
+  for (; q < Q; q += gridDim.x) {
+    const int32_t u = un, i = in;
+    if (q + gridDim.x < Q) {                           // the next query's ids, in flight
+      un = A.qu[q + gridDim.x];
+      in = A.qi[q + gridDim.x];
+    }
+    __syncthreads();                                   // LDS reuse across queries
+    int lane = threadIdx.x & 63;                       // opaque per query (no hoisted addresses)
+    asm volatile("" : "+v"(lane));
+    const int lg = lane >> 4, lc = lane & 15;
+    const bool ok_id = (u >= 0 && u < A.U && i >= 0 && i < A.I);
+    const int32_t uu = ok_id ? u : 0, ii = ok_id ? i : 0;
+    const int64_t pu0 = A.ptr[0][uu], pu1 = A.ptr[0][uu + 1], pi0 = A.ptr[1][ii], pi1 = A.ptr[1][ii + 1];
+    const unsigned long long pkey = (unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii;
+    unsigned long long ph, pk;
+    A.pairs.probe_start(pkey, ph, pk);
+    const int32_t ent = wv ? ii : uu;
+    d4_t U[NU], Rt[NT], hr[NT];
+    double hc[NT], hb = 0.0, gam = 0.0;
+    // NT <= 2: the Gram loads go out before the prologue (one memory latency per query); at
+    // NT >= 3 holding the raw tiles across the prologue spills (MF k=64: 0.42 vs 0.35 ms), so
+    // they are issued after it
+    constexpr bool EARLY = NT <= 2;
+    if constexpr (EARLY) tile_load<NT, EXTRA>(A.gram[wv] + (int64_t)ent * GSP, lg, lc, U, hr, hc, hb);
+    if constexpr (EXTRA) {                             // MF rhs: [other side's embedding ; 1]
+      const float* __restrict__ Eo = A.t[wv ? 0 : 1] + (int64_t)(wv ? uu : ii) * K;
+#pragma unroll
+      for (int p = 0; p < NT; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Rt[p][r] = (double)Eo[16 * p + 4 * r + lg];
+      gam = 1.0;
+    }
+    const int64_t n = ok_id ? (pu1 - pu0) + (pi1 - pi0) : 0;
+    if (n == 0) {
+      if (wv == 0) {
+        if (x_out)
+          for (int a = lane; a < D; a += 64) x_out[q * D + a] = NAN;
+        if (lane == 0) rec[q * M::R] = NAN;
+      }
+      continue;
+    }
+    const double s2n = 2.0 / (double)n;
+    const double rhat_ui = solve_prologue<M, 128>(A, u, i, th, g, sh, w, sW1, sb1);
+    if constexpr (!EXTRA) {                            // NCF rhs from the prologue
+#pragma unroll
+      for (int p = 0; p < NT; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Rt[p][r] = g[wv * Ds + 16 * p + 4 * r + lg];
+    }
+    double cdup, rsum;
+    A.pairs.probe_finish(pkey, ph, pk, cdup, rsum);
+    if (cdup > 0.0) {
+      if (threadIdx.x == 0) {
+        const int slot = atomicAdd(coupled_out, 1);
+        coupled_out[1 + slot] = (int32_t)q;
+      }
+      continue;
+    }
+    if constexpr (!EARLY) tile_load<NT, EXTRA>(A.gram[wv] + (int64_t)ent * GSP, lg, lc, U, hr, hc, hb);
+    tile_factor<NT, EXTRA>(lg, lc, U, Rt, hr, hc, hb, gam, s2n, A.wd, A.damping, xs + wv * Ds, &Pv[wv][0]);
+    __syncthreads();
+    if (wv == 0) solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, xs, w, rec + q * M::R, x_out);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// NCF k <= 16 (side blocks of N = 2k <= 32): one wave per query, the user block in lanes
+// 0..31 and the item block in lanes 32..63, lane c of a half owning column c in registers
+// (right-looking LDL^T, pivot column published through LDS -- solve_blocks_regs' scheme).
+// At N = 32 this takes a third of the tile solve's instructions (no identity tile, no
+// masked rows).  Every global load of a query (next query's ids, list pointers, pair-set
+// probe, both blocks' columns) is issued before the dependent prologue.
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>()))) void k_solve_col(
+    QueryArgs A, int64_t Q, double* __restrict__ rec, double* __restrict__ x_out, int32_t* __restrict__ coupled_out) {
+  constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1, N = Ds;
+  static_assert(M::ncf && 2 * N <= 64, "two side blocks per wave");
+  __shared__ double th[D], g[D], xs[D], Pv[68];
+  __shared__ double sh[4 * K + 8];
+  __shared__ NCFWeights<K> w;
+  __shared__ double sW1[2 * K * K];
+  __shared__ double sb1[K];
+  load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
+  for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
+  for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
+  int64_t q = blockIdx.x;
+  int32_t un = q < Q ? A.qu[q] : 0, in = q < Q ? A.qi[q] : 0;
+  for (; q < Q; q += gridDim.x) {
+    const int32_t u = un, i = in;
+    if (q + gridDim.x < Q) {
+      un = A.qu[q + gridDim.x];
+      in = A.qi[q + gridDim.x];
+    }
+    __syncthreads();
+    // lane-derived values made opaque per query: hoisted out of the query loop, the N column
+    // addresses and lane masks would stay live across it (spills)
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
+    const int b = lane >> 5, c = lane & 31;
+    const bool live = c < N;
+    const bool ok_id = (u >= 0 && u < A.U && i >= 0 && i < A.I);
+    const int32_t uu = ok_id ? u : 0, ii = ok_id ? i : 0;
+    const int64_t pu0 = A.ptr[0][uu], pu1 = A.ptr[0][uu + 1], pi0 = A.ptr[1][ii], pi1 = A.ptr[1][ii + 1];
+    const unsigned long long pkey = (unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii;
+    unsigned long long ph, pk;
+    A.pairs.probe_start(pkey, ph, pk);
+    // column c of this half's block (symmetric: row r of column c = packed (max, min))
+    const double* __restrict__ Gb = A.gram[b] + (int64_t)(b ? ii : uu) * GSP;
+    double col[N];
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      const int hi = r > c ? r : c, lo = r > c ? c : r;
+      col[r] = live ? Gb[tri(hi, lo)] : 0.0;
+    }
+    const int64_t n = ok_id ? (pu1 - pu0) + (pi1 - pi0) : 0;
+    if (n == 0) {
+      if (x_out)
+        for (int a = lane; a < D; a += 64) x_out[q * D + a] = NAN;
+      if (lane == 0) rec[q * M::R] = NAN;
+      continue;
+    }
+    const double s2n = 2.0 / (double)n;
+    const double rhat_ui = solve_prologue<M, 64>(A, u, i, th, g, sh, w, sW1, sb1);
+    double cdup, rsum;
+    A.pairs.probe_finish(pkey, ph, pk, cdup, rsum);
+    if (cdup > 0.0) {
+      if (lane == 0) {
+        const int slot = atomicAdd(coupled_out, 1);
+        coupled_out[1 + slot] = (int32_t)q;
+      }
+      continue;
+    }
+    // H_b = (2/n) Gram_b + (wd + damping) I  (every NCF coordinate is decayed)
+#pragma unroll
+    for (int r = 0; r < N; ++r) col[r] *= s2n;
+#pragma unroll
+    for (int r = 0; r < N; ++r)
+      if (r == c) col[r] += A.wd + A.damping;
+    double y = live ? g[b * N + c] : 0.0;
+    double dinv_own = 0.0;
+    double* __restrict__ Pb = Pv + b * 34;           // column slots [0, 32), y_j at 32, dummy 33
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      Pb[c] = col[j];                                // A[c][j] (= col[j] by symmetry)
+      Pb[c == j ? 32 : 33] = y;                      // y_j is final: the forward solve rides along
+      wave_lds_sync();
+      const double dj = Pb[j];
+      double ij = __builtin_amdgcn_rcp(dj);
+      ij = fma(ij, fma(-dj, ij, 1.0), ij);
+      ij = fma(ij, fma(-dj, ij, 1.0), ij);
+      if (c == j) dinv_own = ij;
+      const double f = c > j ? col[j] * ij : 0.0;
+      const double yj = Pb[32];
+      y = fma(-f, yj, y);
+#pragma unroll
+      for (int r = 0; r < N; ++r)
+        if (r > j) col[r] = fma(-Pb[r], f, col[r]);
+      if (c > j) col[j] = f;
+      wave_lds_sync();
+    }
+    y *= dinv_own;
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) {               // L^T x = D^-1 y
+      const double lo = readlane_d(y, j), hi = readlane_d(y, 32 + j);
+      const double xj = b ? hi : lo;
+      if (c < j) y = fma(-col[j] * dinv_own, xj, y);
+    }
+    if (live) xs[b * N + c] = y;
+    __syncthreads();
+    solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, xs, w, rec + q * M::R, x_out);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -809,8 +1280,6 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
 // C += G^T G; the bias row (sums) and count come from VALU adds.
 // C/D map (f64 16x16x4): col = l & 15, row = (l >> 4) + 4 r.
 // ------------------------------------------------------------------------------------
-typedef double d4_t __attribute__((ext_vector_type(4)));
-
 // both sides' Gram work in one launch: blocks [0, n_items[0]) users, the rest items
 struct GramSides {
   int64_t n_items[2];
@@ -2559,6 +3028,26 @@ constexpr bool use_tps() {
   return !M::ncf && M::Ds <= 17;
 }
 
+// side systems on 16x16 tiles: NCF (Ds = 2k) and MF k >= 32 (k coordinates + the bias)
+template <class M>
+constexpr bool use_tile_solve() {
+  return !use_tps<M>() && (M::ncf ? M::Ds : M::K) % 16 == 0 && (M::ncf ? M::Ds : M::K) <= 64;
+}
+
+// NCF k <= 16: both side blocks in one wave, a column per lane (k_solve_col)
+template <class M>
+constexpr bool use_col_solve() {
+  return M::ncf && 2 * M::Ds <= 64;
+}
+
+// side-system solve (A/B knob FIA_SOLVE): default = k_solve_col (NCF k <= 16) / k_solve_tile,
+// tile = k_solve_tile everywhere, cols = the previous one-column-per-lane k_solve
+static int solve_mode() {
+  static const char* e = getenv("FIA_SOLVE");
+  static const int m = !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "tile") ? 2 : 0;
+  return m;
+}
+
 // MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): run | old
 static const char* mf_score_mode() {
   static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "old";
@@ -2707,6 +3196,22 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       if constexpr (use_tps<M>())
         hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                            c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+    } else if (use_col_solve<M>() && solve_mode() == 0) {
+      if constexpr (use_col_solve<M>()) {
+        static const int64_t genv = getenv("FIA_SOLVE_GRID") ? atoll(getenv("FIA_SOLVE_GRID")) : 0;  // A/B knob
+        const int64_t cap = genv > 0 ? genv : (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;
+        const int64_t g1 = Q < cap ? Q : cap;     // persistent: NCF weights staged once per block
+        hipLaunchKernelGGL(k_solve_col<M>, dim3((unsigned)g1), dim3(64), 0, s, A, Q, c->rec.as<double>(), x_out,
+                           c->coupled.as<int32_t>());
+      }
+    } else if (use_tile_solve<M>() && solve_mode() != 1) {
+      if constexpr (use_tile_solve<M>()) {
+        static const int64_t genv = getenv("FIA_SOLVE_GRID") ? atoll(getenv("FIA_SOLVE_GRID")) : 0;  // A/B knob
+        const int64_t cap = genv > 0 ? genv : (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 8;
+        const int64_t g1 = Q < cap ? Q : cap;     // persistent: NCF weights staged once per block
+        hipLaunchKernelGGL(k_solve_tile<M>, dim3((unsigned)g1), dim3(128), 0, s, A, Q, c->rec.as<double>(), x_out,
+                           c->coupled.as<int32_t>());
+      }
     } else {
       const int64_t g1 = Q < 8192 ? Q : 8192;     // persistent: weights staged once per block
       hipLaunchKernelGGL((k_solve<M, true>), dim3((unsigned)g1), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
