@@ -45,12 +45,13 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6       # MI355X dense FP64 (vector and matrix; tools/mb_f64.hip measures ~70)
 
 CONFIGS = {
     "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m",
-                    scaling="weak"),
+                    scaling="strong"),
     "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp",
-                     scaling="weak"),
+                     scaling="strong"),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
                      k=64, data="20m", scaling="strong"),
     "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "
@@ -67,8 +68,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="ml1m-mf", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default="auto", choices=["auto", "weak", "strong"],
-                    help="N > 1: strong = split the fixed query set over the ranks, weak = a full set per rank "
-                         "(auto: strong for the 20M configs, weak otherwise)")
+                    help="N > 1: strong = split the config's query set over the ranks (auto, every config); "
+                         "weak = a full-size set per rank, ranks > 0 answering SYNTHETIC re-paired queries")
     ap.add_argument("--query-order", default="item", choices=["item", "given"],
                     help="order in which the query set is batched (item-major or the data's order)")
     ap.add_argument("--topk", type=int, default=1)
@@ -91,7 +92,7 @@ def parse(argv=None):
                     help="CPU-baseline worker processes (default: usable host cores, at most 16)")
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto: nccl (RCCL) when every rank has a GPU of its own, gloo when ranks share one")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "score_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args(argv)
 
 
@@ -128,6 +129,48 @@ def load_data(cfg):
     return d, params
 
 
+def solve_kernel(cfg):
+    """The library's side-system solve for this config (models.hip query_impl / bigk.hip)."""
+    k, model = cfg["k"], cfg["model"]
+    if k >= 128 or (model == "NCF" and k >= 64):
+        return "k_bs_trail"              # batched blocked LDL^T panels (+ k_bs_dupd/dfac/back)
+    mode = os.environ.get("FIA_SOLVE", "")
+    if mode == "cols":
+        return "k_solve"
+    if model == "MF" and k <= 16:
+        return "k_solve_tps"
+    if model == "NCF" and k <= 16 and mode != "tile":
+        return "k_solve_col"
+    return "k_solve_tile"
+
+
+def prepare_kernel(cfg):
+    k, model = cfg["k"], cfg["model"]
+    if k >= 128 or (model == "NCF" and k >= 64):
+        return "k_big_gram"
+    return "k_ncf_gram_rows" if model == "NCF" else "k_gram_mf_mfma"
+
+
+def side_dim(model, k):
+    """Coordinates of one side block of H_t: MF k + 1, NCF 2k."""
+    return k + 1 if model == "MF" else 2 * k
+
+
+def solve_flops(model, k, Q):
+    """Algorithmic FP64 flops of the exact solve of Q queries: two side systems of D_s
+    coordinates each, LDL^T (D^3/3 multiply-adds) + forward and backward solves (D^2)."""
+    Dd = float(side_dim(model, k))
+    return 2.0 * Q * (2.0 * Dd ** 3 / 3.0 + 2.0 * Dd * Dd)
+
+
+def prepare_flops(model, k, N):
+    """Entity Gram caches: per rating and side a symmetric rank-1 update, D_s(D_s+1)/2
+    multiply-adds (+ for NCF the ~12 k^2 flops of the per-rating MLP)."""
+    Dd = float(side_dim(model, k))
+    per = Dd * (Dd + 1.0) + (12.0 * k * k if model == "NCF" else 0.0)
+    return 2.0 * N * per
+
+
 def score_kernel(cfg, K=1):
     """The library's scoring kernel for this config (the dispatch in models.hip query_impl /
     bigk.hip query_big_impl, including their environment switches)."""
@@ -138,7 +181,7 @@ def score_kernel(cfg, K=1):
         return "k_score_ncf"
     if k <= 16:
         mode = os.environ.get("FIA_MF_SCORE", "old")
-        return {"run": "k_score_mf_run", "res": "k_score_mf_res"}.get(mode, "k_score_mf")
+        return "k_score_mf_run" if mode == "run" else "k_score_mf"
     if k in (32, 64) and K <= 1 and not os.environ.get("FIA_NO_MFMA_SCORE"):
         return "k_score_mf_mfma"
     return "k_score_grouped_mf"
@@ -311,17 +354,32 @@ def rank_query_items(qu, qi, train, I, rank, stats=None):
 
 
 def load_traffic(path, config, kernel):
-    """PMC HBM bytes per launch of `kernel` for `config` (profiles/score_traffic.json), or None."""
+    """PMC HBM bytes per launch of `kernel` for `config`, or None.  profiles/traffic.json:
+    {config: {kernel: entry}} (tools/traffic_json.py); the round-2 layout {config: entry}
+    is read too."""
     if not os.path.exists(path):
         return None
     try:
-        tj = json.load(open(path))
-        tj = tj.get(config, {}) if "config" not in tj else tj
-        if tj.get("config") == config and tj.get("kernel", "") == kernel:
+        tj = json.load(open(path)).get(config, {})
+        if tj.get("kernel") == kernel:
             return tj
+        e = tj.get(kernel)
+        return e if isinstance(e, dict) and e.get("kernel") == kernel else None
     except Exception:
         return None
-    return None
+
+
+def compulsory_bytes(cfg, qu, qi, deg_u, deg_i, bounds):
+    """Bytes the scoring kernel cannot avoid, per launch (mean over the batches): its outputs
+    (8 B influence + 4 B train row per related rating) and every list entry of the batch's
+    users and items read once (4 B row + 4 B other id + 4 B rating)."""
+    tot = 0.0
+    for b0, b1 in zip(bounds[:-1], bounds[1:]):
+        u, i = qu[b0:b1], qi[b0:b1]
+        out = 12.0 * float(deg_u[u].sum() + deg_i[i].sum())
+        lists = 12.0 * float(deg_u[np.unique(u)].sum() + deg_i[np.unique(i)].sum())
+        tot += out + lists
+    return tot / max(len(bounds) - 1, 1)
 
 
 def main():
@@ -436,9 +494,13 @@ def main():
     gdev = dev if backend == "nccl" else torch.device("cpu")
     tg = TopKGather(all_sizes, K, gdev) if world > 1 else None
 
+    # a rank answering a shard of the query set builds only its users'/items' caches
+    # (fia_prepare_for; small k: marked on the device, no host round trip); the full set
+    # builds every cache
+    sharded = shard_of > 1
     def compute():
-        if big_k:
-            ctx.prepare_for(qu, qi)    # caches for this GPU's users/items only (fia_prepare_for)
+        if big_k or sharded:
+            ctx.prepare_for(qu, qi)
         else:
             ctx.prepare()
         for b0, b1, qb_u, qb_i, off_b, tot_b in batches:
@@ -493,7 +555,11 @@ def main():
             compute()
         torch.cuda.synchronize(dev)
 
-    ctx.set_profiling(True, phases=("score",))
+    # the step's dominant phase (instrumented steps above) is priced by the roofline; its
+    # launches and the scoring kernel's are timed by HIP events over the timed region
+    per_step = {p: v[0] / n_instr for p, v in phases.items()}
+    dom = max(("prepare", "solve", "score"), key=lambda p: per_step.get(p, 0.0))
+    ctx.set_profiling(True, phases=tuple(sorted({"score", dom})))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -520,23 +586,60 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     node_queries = int(sum(all_sizes))
     value = node_queries * args.steps / elapsed
-    score_ms = timed["score"][0] / max(timed["score"][1], 1)            # per launch, timed region
-    if timed["score"][1] == 0:
-        # graph replay: the library's events are not re-recorded by a replayed graph, so the
-        # kernel time comes from the instrumented eager steps
-        score_ms = phases["score"][0] / max(phases["score"][1], 1)
+
+    def timed_ms(phase):
+        # per launch over the timed region (graph replay: events are not re-recorded, so the
+        # instrumented eager steps stand in)
+        t = timed.get(phase, (0.0, 0))
+        if t[1] == 0:
+            t = phases.get(phase, (0.0, 0))
+        return t[0] / max(t[1], 1)
+
+    # the scoring kernel against HBM: PMC bytes per launch (profiles/traffic.json) over its
+    # event time; compulsory bytes = its outputs + every list entry of the batch read once
+    score_ms = timed_ms("score")
     kern = score_kernel(cfg, K)
     alg_bytes = float(bytes_per_query(cfg["model"], k, n_q).sum()) / len(batches)   # mean per launch
     tj = load_traffic(args.traffic_json, args.config, kern)
     traffic = tj.get("hbm_bytes_per_launch") if tj else None
+    deg_u = np.bincount(tu, minlength=U).astype(np.float64)
+    deg_i = np.bincount(ti, minlength=I).astype(np.float64)
+    comp = compulsory_bytes(cfg, qu_np, qi_np, deg_u, deg_i, bounds)
     achieved = traffic / (score_ms * 1e-3) / 1e9 if traffic else None
-    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
-                "kernel": kern, "kernel_ms": score_ms,
-                "source": ("rocprofv3 PMC (FETCH_SIZE x 2 + WRITE_SIZE) per launch, %s" % os.path.relpath(
-                    args.traffic_json, ROOT)) if traffic else "no PMC traffic recorded for this config/kernel",
-                "algorithmic": {"model": "SURVEY.md 8d (gathered rows counted once per query)",
-                                "bytes_per_launch": alg_bytes, "gbs": alg_bytes / (score_ms * 1e-3) / 1e9}}
+    score_hbm = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
+                 "compulsory_bytes": comp, "traffic_over_compulsory": traffic / comp if traffic else None,
+                 "kernel": kern, "kernel_ms": score_ms,
+                 "source": ("rocprofv3 PMC (FETCH_SIZE x 2 + WRITE_SIZE) per launch, %s" % os.path.relpath(
+                     args.traffic_json, ROOT)) if traffic else "no PMC traffic recorded for this config/kernel",
+                 "algorithmic": {"model": "SURVEY.md 8d (gathered rows counted once per query)",
+                                 "bytes_per_launch": alg_bytes, "gbs": alg_bytes / (score_ms * 1e-3) / 1e9}}
+    if dom == "score":
+        roofline = dict(score_hbm, phase="score")
+    else:
+        # a compute phase: algorithmic FP64 flops per launch over its event time
+        ph_ms = timed_ms(dom)
+        if dom == "solve":
+            dk = solve_kernel(cfg)
+            flops = solve_flops(cfg["model"], k, Q) / len(batches)
+            fmodel = "2 side systems per query of D_s = %d: LDL^T 2D^3/3 + solves 2D^2 flops" % side_dim(cfg["model"], k)
+        else:
+            dk = prepare_kernel(cfg)
+            flops = prepare_flops(cfg["model"], k, int(tu.size))
+            fmodel = "per rating and side: Gram rank-1 update D_s(D_s+1) flops (+ NCF MLP 12 k^2)"
+        dtj = load_traffic(args.traffic_json, args.config, dk)
+        dtraffic = dtj.get("hbm_bytes_per_launch") if dtj else None
+        tfs = flops / (ph_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": tfs / FP64_PEAK_TFS, "traffic": dtraffic, "phase": dom, "kernel": dk, "kernel_ms": ph_ms,
+                    "dtype": "f64", "flops_per_launch": flops, "flop_model": fmodel,
+                    "peak_note": "MI355X dense FP64; f64 MFMA and f64 VALU issue to the same DP units (DESIGN.md "
+                                 "section 6), so this one peak bounds both",
+                    "traffic_gbs": dtraffic / (ph_ms * 1e-3) / 1e9 if dtraffic else None,
+                    "score_hbm": score_hbm}
+    workload = cfg["workload"]
+    if world > 1 and scaling == "weak":
+        workload += " -- WEAK scaling: ranks > 0 answer synthetic re-paired queries of the same shape"
     out = {
         "metric": "influence queries/sec (whole node) + % HBM roofline, MF k=16 ML-1M-ex"
         if args.config == "ml1m-mf" else "influence queries/sec (whole node), " + cfg["workload"],
@@ -545,7 +648,9 @@ def main():
         "dtype": "f64",
         "data": "synthetic train ratings of the reference shape (train file not distributed) + the reference's "
                 "real held-out test pairs (20M: synthetic held-out pairs); synthetic parameters",
-        "config": {"workload": cfg["workload"], "model": cfg["model"], "k": k, "queries_per_rank": all_sizes,
+        "config": {"workload": workload, "scope": "%d GPU%s (value = all ranks' queries / max-over-ranks time)" % (
+                       world, "" if world == 1 else "s"),
+                   "model": cfg["model"], "k": k, "queries_per_rank": all_sizes,
                    "node_queries_per_step": node_queries, "n_train": int(tu.size),
                    "related_ratings_rank0_step": int(total), "topk": K, "query_batches": len(batches),
                    "query_order": args.query_order, "shard_of": shard_of, "hip_graph": use_graph,

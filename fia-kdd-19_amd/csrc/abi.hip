@@ -68,6 +68,24 @@ int hip_fail(fia_ctx* c, hipError_t e, const char* where) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Every stream-taking entry point starts here.  DevBuf regrows free their old block in
+// order on the CALLING stream; when the caller switches streams, kernels of the previous
+// call may still be queued on the old one, so the device is synchronised first (rare: a
+// context normally sees one stream).  A capturing stream cannot synchronise -- and cannot
+// regrow a buffer either (DevBuf::reserve refuses), so nothing is freed under it.
+hipError_t enter_stream(fia_ctx* c, hipStream_t s) {
+  if (c->has_stream && c->stream != s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) return e;
+    }
+  }
+  c->stream = s;
+  c->has_stream = true;
+  return hipSuccess;
+}
+
 }  // namespace
 
 extern "C" {
@@ -173,6 +191,7 @@ int fia_build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* 
     if (c->p.valid && (c->p.U != U || c->p.I != I))
       return fail(c, FIA_ERR_INVALID, "num_users/num_items differ from the registered params");
     DeviceGuard g(c->device);
+    if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_build_index");
     std::string why;
     hipError_t e = fia::build_index(c, N, U, I, user, item, rating, as_stream(stream), why);
     c->prepared = false;
@@ -191,6 +210,7 @@ int fia_prepare(fia_ctx* c, void* stream) {
     if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
+    if (hipError_t es = enter_stream(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare");
     bool unsup = false;
     fia::phase_begin(c, 0, s);
     hipError_t e = fia::prepare_model(c, s, unsup);
@@ -213,13 +233,14 @@ int fia_prepare_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
     if (Q > 0 && (!qu || !qi)) return fail(c, FIA_ERR_INVALID, "null query array");
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
+    if (hipError_t es = enter_stream(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare_for");
     bool unsup = false;
     hipError_t e;
     fia::phase_begin(c, 0, s);
     if (fia::big_supported(c->p.model, c->p.k)) {
       e = fia::prepare_big(c, Q, qu, qi, s);
     } else {
-      e = fia::prepare_model(c, s, unsup);   // small k: the caches are cheap, build them all
+      e = fia::prepare_model_for(c, Q, qu, qi, s, unsup);   // small k: marked entities only, no sync
     }
     fia::phase_end(c, 0, s);
     c->prepared = false;
@@ -240,7 +261,8 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     if (!offsets || (Q > 0 && (!qu || !qi))) return fail(c, FIA_ERR_INVALID, "null query array");
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
-    hipError_t e;
+    hipError_t e = enter_stream(c, s);
+    if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
     if (total_out) {
       e = c->flag.reserve(64, s);
       if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
@@ -249,6 +271,7 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     }
     e = fia::count_related(c, Q, qu, qi, offsets, s);
     if (e == hipSuccess && total_out) e = fia::check_cover(c, Q, qu, qi, c->flag.as<int32_t>() + 2, s);
+    if (e == hipSuccess && total_out) e = fia::check_cover_small(c, Q, qu, qi, c->flag.as<int32_t>() + 2, s);
     if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
     if (total_out) {
       int32_t flags[4] = {0, 0, 0, 0};
@@ -273,6 +296,7 @@ int fia_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, con
     if (Q < 0 || Q >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "num_queries out of range");
     if (Q > 0 && (!qu || !qi || !offsets || !rel_idx)) return fail(c, FIA_ERR_INVALID, "null array");
     DeviceGuard g(c->device);
+    if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_related");
     hipError_t e = fia::write_related(c, Q, qu, qi, offsets, rel_idx, as_stream(stream));
     if (e != hipSuccess) return hip_fail(c, e, "fia_related");
     return FIA_OK;
@@ -293,6 +317,7 @@ int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
     if (K > 0 && (!topk_pos || !topk_idx || !topk_val)) return fail(c, FIA_ERR_INVALID, "null top-K output");
     if (Q == 0) return FIA_OK;
     DeviceGuard g(c->device);
+    if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
     const int64_t max_chunks = 2 * Q + total_rel / fia::kChunk + 1;
     bool unsup = false;
     hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,

@@ -1915,6 +1915,7 @@ bool big_supported(int model, int k) {
 }
 
 hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s) {
+  c->small_subset = false;
 #define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_big_impl<T>(c, Q, qu, qi, s);
   FIA_BIG_CASES(X)
 #undef X

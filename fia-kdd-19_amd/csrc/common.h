@@ -36,7 +36,10 @@ constexpr int kBigQueryBlock = 8;        // ... large k (register-resident per-q
 // Device buffer with grow-on-demand capacity (never shrinks), allocated from the
 // device's stream-ordered pool on the context's stream: growing a buffer frees the old
 // block in stream order (kernels already queued on `s` still read it) and allocates
-// the new one behind them -- no device-wide synchronisation on the query path.  A
+// the new one behind them -- no device-wide synchronisation on the query path.  Work
+// queued on ANOTHER stream is covered by the ABI: a call arriving on a different stream
+// than the context's previous call first synchronises the device (fia_ctx::stream,
+// abi.hip enter_stream), so a stream-ordered free never overtakes a reader there.  A
 // regrown buffer gets 25 % headroom so a slowly growing batch does not regrow it
 // every call.  Contents are not preserved.
 struct DevBuf {
@@ -44,6 +47,11 @@ struct DevBuf {
   size_t bytes = 0;
   hipError_t reserve(size_t want, hipStream_t s) {
     if (want <= bytes && ptr) return hipSuccess;
+    // a regrow inside a graph capture would free a block allocated outside the graph:
+    // buffers must be sized by an eager call before capture
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return hipErrorStreamCaptureUnsupported;
     size_t cap = want < 256 ? 256 : want;
     if (ptr) {
       const size_t grown = bytes + bytes / 4;
@@ -200,6 +208,7 @@ struct fia_ctx {
   fia::DevBuf slot[2];    // int32 [n_entity] Gram cache slot (-1 = not cached) after fia_prepare_for
   fia::DevBuf mark;       // uint8 [U + I] entities referenced by the fia_prepare_for queries
   bool subset = false;    // caches cover only the fia_prepare_for entities (large-k models)
+  bool small_subset = false;   // small k after fia_prepare_for: Grams of the `mark`ed entities only
   fia::DevBuf bitems[2], bcomb[2];   // large-k Gram work lists {entity, start, len, slot}
   int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0}, n_bcache[2] = {0, 0};
   uint64_t bitems_version = ~0ull;
@@ -210,6 +219,10 @@ struct fia_ctx {
   fia::DevBuf cpllist;    // int32 [1 + Q]  {count, q ...} coupled full systems
   fia::DevBuf lscr;       // double LDL^T factor scratch, one slab per resident solve workgroup
   int num_cus = 0;
+  // the stream of the previous call (a switch synchronises first: DevBuf frees are ordered
+  // on the calling stream only)
+  hipStream_t stream = nullptr;
+  bool has_stream = false;
   int score_mode = -1;    // scoring schedule: -1 auto, 0 per-query chunks, 1 entity-shared (FIA_SCORE)
   unsigned profiling = 0;   // bit p: record phase p (fia_set_profiling)
   fia::PhaseEvents events;
@@ -238,6 +251,11 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
 
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported);
+// small k: caches of the queries' users and items only (fia_prepare_for); marks in c->mark
+hipError_t prepare_model_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s,
+                             bool& unsupported);
+hipError_t check_cover_small(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag,
+                             hipStream_t s);
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                        int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                        int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,

@@ -288,8 +288,10 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   // the last tile to finish resets the tile words and the counters for the next launch
   __syncthreads();
   if (threadIdx.x == 0) {
-    // (no fence: the tile words this block read were consumed before this point, and the
-    // outputs are read by later kernels only)
+    // this thread published the block's tile words: wait for those stores to be performed
+    // before counting the block done, so the last block's reset cannot be overtaken by a
+    // straggling publish (the outputs are read by later kernels only)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned done = atomicAdd(&tctr[1], 1u);
     if (done == ntiles - 1) {
       for (unsigned t = 0; t < ntiles; ++t)
@@ -390,6 +392,8 @@ __global__ __launch_bounds__(kScanThreads) void k_group_scan(
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    // the block's tile-word stores performed before it counts itself done (see k_query_scan)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned done = atomicAdd(&tctr[1], 1u);
     if (done == ntiles - 1) {
       for (unsigned w = 0; w < 2 * ntiles; ++w)

@@ -749,7 +749,11 @@ __device__ __forceinline__ double col_sum4(double x) {
 // waves per SIMD the tile solve is compiled for (registers: 4 tiles of state per 16 coordinates)
 template <class M>
 constexpr int col_waves() {
-  return M::Ds <= 16 ? 4 : 3;
+#ifdef FIA_COL_WAVES
+  return M::Ds <= 16 ? 4 : FIA_COL_WAVES;
+#else
+  return M::Ds <= 16 ? 4 : 2;     // N = 32: two 32-row columns per lane (128 VGPRs of matrix)
+#endif
 }
 
 template <class M>
@@ -1031,112 +1035,337 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(tile_waves<
 }
 
 // ------------------------------------------------------------------------------------
-// NCF k <= 16 (side blocks of N = 2k <= 32): one wave per query, the user block in lanes
-// 0..31 and the item block in lanes 32..63, lane c of a half owning column c in registers
-// (right-looking LDL^T, pivot column published through LDS -- solve_blocks_regs' scheme).
-// At N = 32 this takes a third of the tile solve's instructions (no identity tile, no
-// masked rows).  Every global load of a query (next query's ids, list pointers, pair-set
-// probe, both blocks' columns) is issued before the dependent prologue.
+// NCF k <= 16 (side blocks of N = 2k <= 32): QW = 32 / k queries per wave.  A side system
+// lives in LS = N / 2 lanes (the user block, then the item block, of each query), lane t
+// owning columns t and t + LS in registers: a right-looking LDL^T in which step j publishes
+// the pivot column through LDS (every lane stores its two entries A[c][j] = col_c[j]) and
+// reads it back as uniform-address ds_read_b128 broadcasts, each value feeding TWO FMAs (one
+// per owned column: half the LDS traffic per FMA of a column-per-lane layout, which is what
+// bounds this solve).  The forward solve rides along; the backward solve broadcasts x_j by
+// DPP row_newbcast.  Every global load of a query is issued before its prologue.
 // ------------------------------------------------------------------------------------
+// sum over the 2 * LS lanes of one query (its two side systems), every lane of it gets the
+// same bits: LS = 16 -- a 16-lane row sum, then rows 2h + 1 and 2h; LS = 8 -- a row sum
+template <int LS>
+__device__ __forceinline__ double sys_sum(double x) {
+  x = row_sum16(x);
+  if constexpr (LS == 16) {
+    const long long b = __double_as_longlong(x);
+    const unsigned lo = (unsigned)(b & 0xffffffffll), hi = (unsigned)(b >> 32);
+    const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    x = __longlong_as_double(((long long)h16[0] << 32) | l16[0]) +
+        __longlong_as_double(((long long)h16[1] << 32) | l16[1]);
+  } else {
+    static_assert(LS == 8, "k = 8 or 16");
+  }
+  return x;
+}
+
+template <int N, int J>
+__device__ __forceinline__ double bcast_sys(double x, int t) {
+  // lane (J % LS) of each LS-lane system; LS = 16: one system per DPP row, LS = 8: two
+  constexpr int LS = N / 2;
+  if constexpr (LS == 16) {
+    return dpp_d<0x150 + (J % 16)>(x);
+  } else {
+    static_assert(LS == 8, "k = 8 or 16");
+    const double lo = dpp_d<0x150 + (J % 8)>(x), hi = dpp_d<0x150 + 8 + (J % 8)>(x);
+    return t >= 0 && (threadIdx.x & 8) ? hi : lo;
+  }
+}
+
+// NCF prologue for QW queries per wave (LQ = 64 / QW lanes per query): theta_t, v and r-hat
+// (ncf:102-145, 181-191; gnn:155) into th[h][D] / g[h][D]; rh[h] = r-hat(u,i)
+template <class M, int QW>
+__device__ void ncf_prologue_multi(const QueryArgs& A, const int32_t* __restrict__ uq, const int32_t* __restrict__ iq,
+                                   double (*th)[M::D], double (*g)[M::D], double (*sh)[4 * M::K + 8],
+                                   const NCFWeights<M::K>& w, const double* __restrict__ sW1,
+                                   const double* __restrict__ sb1, double* __restrict__ rh) {
+  constexpr int K = M::K, Ds = M::Ds, H2 = K / 2, LQ = 64 / QW;
+  static_assert(2 * K <= LQ, "one lane per g entry");
+  const int h = threadIdx.x / LQ, a = threadIdx.x % LQ;
+  const int32_t u = uq[h], i = iq[h];
+  double* __restrict__ z1 = sh[h];
+  double* __restrict__ d2 = sh[h] + K;
+  double* __restrict__ d1 = sh[h] + 2 * K;
+  if (a < K) {
+    th[h][a] = A.t[0][(int64_t)u * K + a];
+    th[h][K + a] = A.t[2][(int64_t)u * K + a];
+    th[h][Ds + a] = A.t[1][(int64_t)i * K + a];
+    th[h][Ds + K + a] = A.t[3][(int64_t)i * K + a];
+    z1[a] = A.l1[0][(int64_t)u * K + a] + A.l1[1][(int64_t)i * K + a] + sb1[a];
+  }
+  wave_lds_sync();
+  double part = 0.0;
+  if (a < H2) {
+    double z2 = w.b2[a];
+#pragma unroll
+    for (int c = 0; c < K; ++c) z2 = fma(w.W2[c * H2 + a], z1[c] > 0.0 ? z1[c] : 0.0, z2);
+    const bool on = z2 > 0.0;
+    d2[a] = on ? w.W3[a] : 0.0;
+    part = on ? w.W3[a] * z2 : 0.0;
+  }
+  if (a < K) part += w.W3[H2 + a] * th[h][K + a] * th[h][Ds + K + a];
+#pragma unroll
+  for (int off = LQ / 2; off > 0; off >>= 1) part += __shfl_xor(part, off);
+  if (a == 0) rh[h] = part + (double)A.t[9][0];
+  wave_lds_sync();
+  if (a < K) {
+    double t = 0.0;
+#pragma unroll
+    for (int dd = 0; dd < H2; ++dd) t = fma(w.W2[a * H2 + dd], d2[dd], t);
+    d1[a] = z1[a] > 0.0 ? t : 0.0;
+  }
+  wave_lds_sync();
+  if (a < 2 * K) {
+    // rows a < K: W1[:k] (Pm part, user block); rows a >= K: W1[k:] (Qm part, item block)
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) s = fma(sW1[a * K + c], d1[c], s);
+    if (a < K) g[h][a] = s; else g[h][Ds + (a - K)] = s;
+  }
+  if (a < K) {
+    g[h][K + a] = w.W3[H2 + a] * th[h][Ds + K + a];        // d r/d Pg_u = W3g * Qg_i
+    g[h][Ds + K + a] = w.W3[H2 + a] * th[h][K + a];        // d r/d Qg_i = W3g * Pg_u
+  }
+  wave_lds_sync();
+}
+
+// Pivot slots of one system: [0, N) the pivot column, N y_J, N + 1 1/d_J.  Every lane
+// writes its two entries of column J; the owners of row J add y_J and 1/d_J.
+template <int N, int J>
+__device__ __forceinline__ void ncf2_publish(const double (&c0)[N], const double (&c1)[N], double y0, double y1,
+                                             int t, double* __restrict__ Pb) {
+  constexpr int LS = N / 2;
+  const int ca = t, cb = t + LS;
+  Pb[ca] = c0[J];                                  // A[ca][J] = col_ca[J] (symmetric)
+  Pb[cb] = c1[J];
+  if (ca == J || cb == J) {                        // the diagonal's owner: y_J and 1/d_J
+    const double dj = ca == J ? c0[J] : c1[J];
+    double ij = __builtin_amdgcn_rcp(dj);
+    ij = fma(ij, fma(-dj, ij, 1.0), ij);
+    ij = fma(ij, fma(-dj, ij, 1.0), ij);
+    Pb[N] = ca == J ? y0 : y1;
+    Pb[N + 1] = ij;
+  }
+}
+
+// Step J, software-pipelined: the pivot data of step J are in LDS; row J + 1 is updated
+// first and published (with y_{J+1} and 1/d_{J+1}) before the remaining FMAs of step J, so
+// the next step's LDS round trip overlaps them.
+template <int N, int J>
+__device__ __forceinline__ void ncf2_step(double (&c0)[N], double (&c1)[N], double& y0, double& y1,
+                                          double& di0, double& di1, int t, double* __restrict__ P0,
+                                          double* __restrict__ P1) {
+  constexpr int LS = N / 2;
+  const int ca = t, cb = t + LS;
+  double* __restrict__ Pb = (J & 1) ? P1 : P0;
+  double* __restrict__ Pn = (J & 1) ? P0 : P1;
+  wave_lds_sync();
+  const double ij = Pb[N + 1], yj = Pb[N];
+  if (ca == J) di0 = ij;
+  if (cb == J) di1 = ij;
+  const double f0 = ca > J ? c0[J] * ij : 0.0;
+  const double f1 = cb > J ? c1[J] * ij : 0.0;
+  y0 = fma(-f0, yj, y0);
+  y1 = fma(-f1, yj, y1);
+  if constexpr (J + 1 < N) {
+    const double p = Pb[J + 1];
+    c0[J + 1] = fma(-p, f0, c0[J + 1]);
+    c1[J + 1] = fma(-p, f1, c1[J + 1]);
+    ncf2_publish<N, J + 1>(c0, c1, y0, y1, t, Pn);
+  }
+#pragma unroll
+  for (int r = J + 2; r < N; ++r) {
+    const double p = Pb[r];
+    c0[r] = fma(-p, f0, c0[r]);
+    c1[r] = fma(-p, f1, c1[r]);
+  }
+  if (ca > J) c0[J] = f0;                          // L[ca][J]
+  if (cb > J) c1[J] = f1;
+  // materialise this step's updates here (hipcc otherwise sinks each row's FMA to the step
+  // that first needs it and keeps every step's pivot values live: spills)
+#pragma unroll
+  for (int r = J; r < N; ++r) asm volatile("" : "+v"(c0[r]), "+v"(c1[r]));
+  asm volatile("" : "+v"(y0), "+v"(y1));
+}
+
+template <int N, int J>
+__device__ __forceinline__ void ncf2_steps(double (&c0)[N], double (&c1)[N], double& y0, double& y1, double& di0,
+                                           double& di1, int t, double* __restrict__ P0, double* __restrict__ P1) {
+  if constexpr (J < N) {
+    ncf2_step<N, J>(c0, c1, y0, y1, di0, di1, t, P0, P1);
+    ncf2_steps<N, J + 1>(c0, c1, y0, y1, di0, di1, t, P0, P1);
+  }
+}
+
+template <int N, int J>
+__device__ __forceinline__ void ncf2_back(const double (&c0)[N], const double (&c1)[N], double& y0, double& y1,
+                                          double di0, double di1, int t) {
+  // L^T x = D^-1 y from the last row: x_J (final in its owner lane) is broadcast to the
+  // system's lanes, every lane with a column c < J removes L[J][c] x_J
+  if constexpr (J >= 0) {
+    constexpr int LS = N / 2;
+    const double own = (J < LS) ? y0 : y1;
+    const double xj = bcast_sys<N, J>(own, t);
+    const int ca = t, cb = t + LS;
+    if (ca < J) y0 = fma(-c0[J] * di0, xj, y0);
+    if (cb < J) y1 = fma(-c1[J] * di1, xj, y1);
+    ncf2_back<N, J - 1>(c0, c1, y0, y1, di0, di1, t);
+  }
+}
+
 template <class M>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>()))) void k_solve_col(
     QueryArgs A, int64_t Q, double* __restrict__ rec, double* __restrict__ x_out, int32_t* __restrict__ coupled_out) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1, N = Ds;
-  static_assert(M::ncf && 2 * N <= 64, "two side blocks per wave");
-  __shared__ double th[D], g[D], xs[D], Pv[68];
-  __shared__ double sh[4 * K + 8];
+  constexpr int LS = N / 2, NSYS = 64 / LS, QW = NSYS / 2, PSTR = N + 2;
+  static_assert(M::ncf && (N == 16 || N == 32), "NCF k = 8 or 16");
+  __shared__ double th[QW][D], g[QW][D], sh[QW][4 * K + 8], rh[QW], s_cd[QW];
+  __shared__ int32_t s_u[QW], s_i[QW];
+  __shared__ int64_t s_n[QW];
+  __shared__ double Pv[2][NSYS * PSTR];
   __shared__ NCFWeights<K> w;
   __shared__ double sW1[2 * K * K];
   __shared__ double sb1[K];
   load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
   for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
   for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
-  int64_t q = blockIdx.x;
-  int32_t un = q < Q ? A.qu[q] : 0, in = q < Q ? A.qi[q] : 0;
-  for (; q < Q; q += gridDim.x) {
-    const int32_t u = un, i = in;
-    if (q + gridDim.x < Q) {
-      un = A.qu[q + gridDim.x];
-      in = A.qi[q + gridDim.x];
-    }
+  const int64_t stride = (int64_t)gridDim.x * QW;
+#ifdef FIA_STAMPS
+  long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long t_prev = __builtin_amdgcn_s_memtime();
+  int iters = 0;
+#define STAMP(k) do { const long long t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - t_prev; t_prev = t_; } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+  for (int64_t q0 = (int64_t)blockIdx.x * QW; q0 < Q; q0 += stride) {
     __syncthreads();
-    // lane-derived values made opaque per query: hoisted out of the query loop, the N column
+#ifdef FIA_STAMPS
+    ++iters;
+#endif
+    STAMP(0);
+    // lane-derived values made opaque per iteration: hoisted out of the loop, the 2N column
     // addresses and lane masks would stay live across it (spills)
     int lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
-    const int b = lane >> 5, c = lane & 31;
-    const bool live = c < N;
-    const bool ok_id = (u >= 0 && u < A.U && i >= 0 && i < A.I);
-    const int32_t uu = ok_id ? u : 0, ii = ok_id ? i : 0;
-    const int64_t pu0 = A.ptr[0][uu], pu1 = A.ptr[0][uu + 1], pi0 = A.ptr[1][ii], pi1 = A.ptr[1][ii + 1];
-    const unsigned long long pkey = (unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii;
-    unsigned long long ph, pk;
-    A.pairs.probe_start(pkey, ph, pk);
-    // column c of this half's block (symmetric: row r of column c = packed (max, min))
-    const double* __restrict__ Gb = A.gram[b] + (int64_t)(b ? ii : uu) * GSP;
-    double col[N];
+    const int sys = lane / LS, t = lane % LS, qs = sys >> 1, sd = sys & 1;
+    // lane h < QW: query q0 + h -- ids, related count, first pair-set probe
+    unsigned long long pk = 0, ph = 0, pv = 0;
+    if (lane < QW) {
+      const int64_t q = q0 + lane;
+      const int32_t u = q < Q ? A.qu[q] : -1, i = q < Q ? A.qi[q] : -1;
+      const bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
+      const int32_t uu = ok ? u : 0, ii = ok ? i : 0;
+      const int64_t nn = ok ? (A.ptr[0][uu + 1] - A.ptr[0][uu]) + (A.ptr[1][ii + 1] - A.ptr[1][ii]) : 0;
+      pk = (unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii;
+      A.pairs.probe_start(pk, ph, pv);
+      s_u[lane] = uu;                                // clamped ids (n = 0 for invalid ones)
+      s_i[lane] = ii;
+      s_n[lane] = nn;
+    }
+    wave_lds_sync();
+    STAMP(1);
+    const int32_t ent = sd ? s_i[qs] : s_u[qs];
+    const double* __restrict__ Gb = A.gram[sd] + (int64_t)ent * GSP;
+    const int ca = t, cb = t + LS;
+    // the prologue first: holding the 2N loaded columns across it spills
+    ncf_prologue_multi<M, QW>(A, s_u, s_i, th, g, sh, w, sW1, sb1, rh);
+    STAMP(2);
+    double c0[N], c1[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) {
-      const int hi = r > c ? r : c, lo = r > c ? c : r;
-      col[r] = live ? Gb[tri(hi, lo)] : 0.0;
+      const int h0 = r > ca ? r : ca, l0 = r > ca ? ca : r;
+      const int h1 = r > cb ? r : cb, l1 = r > cb ? cb : r;
+      c0[r] = Gb[tri(h0, l0)];
+      c1[r] = Gb[tri(h1, l1)];
     }
-    const int64_t n = ok_id ? (pu1 - pu0) + (pi1 - pi0) : 0;
-    if (n == 0) {
-      if (x_out)
-        for (int a = lane; a < D; a += 64) x_out[q * D + a] = NAN;
-      if (lane == 0) rec[q * M::R] = NAN;
-      continue;
+    const int64_t n = s_n[qs];
+    // H_b = (2/n) Gram_b + (wd + damping) I  (every NCF coordinate is decayed); n = 0: the
+    // system is garbage and its query writes NaN below
+    const double s2n = n > 0 ? 2.0 / (double)n : 0.0;
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      c0[r] *= s2n;
+      c1[r] *= s2n;
     }
-    const double s2n = 2.0 / (double)n;
-    const double rhat_ui = solve_prologue<M, 64>(A, u, i, th, g, sh, w, sW1, sb1);
-    double cdup, rsum;
-    A.pairs.probe_finish(pkey, ph, pk, cdup, rsum);
-    if (cdup > 0.0) {
-      if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < N; ++r) {
+      if (r == ca) c0[r] += A.wd + A.damping;
+      if (r == cb) c1[r] += A.wd + A.damping;
+    }
+    double y0 = g[qs][sd * N + ca], y1 = g[qs][sd * N + cb];
+    const double g0 = y0, g1 = y1;
+    ncf2_publish<N, 0>(c0, c1, y0, y1, t, &Pv[0][sys * PSTR]);
+#ifdef FIA_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(c0[N - 1]), "+v"(c1[N - 1]));
+#endif
+    STAMP(3);
+    double di0 = 0.0, di1 = 0.0;
+    ncf2_steps<N, 0>(c0, c1, y0, y1, di0, di1, t, &Pv[0][sys * PSTR], &Pv[1][sys * PSTR]);
+    STAMP(4);
+    y0 *= di0;
+    y1 *= di1;
+    ncf2_back<N, N - 1>(c0, c1, y0, y1, di0, di1, t);
+    STAMP(5);
+    if (lane < QW) {                                 // is the test pair a train row?
+      double cdup, rsum;
+      A.pairs.probe_finish(pk, ph, pv, cdup, rsum);
+      s_cd[lane] = cdup;
+    }
+    wave_lds_sync();
+    // ---- record + x_out, lane-parallel: this lane holds x at coordinates ca, cb of side sd
+    // of query qs (record layout: solve_epilogue) ----
+    {
+      const int64_t q = q0 + qs;
+      const int64_t nn = s_n[qs];
+      const bool live_q = q < Q && nn > 0 && !(s_cd[qs] > 0.0);
+      constexpr int H2 = K / 2;
+      // x . theta over the decayed coordinates (all of NCF's) and x . v, summed over the query's
+      // two systems (2 LS lanes)
+      double cq = fma(y0, th[qs][sd * N + ca], y1 * th[qs][sd * N + cb]);
+      double xv = fma(y0, g0, y1 * g1);
+      cq = sys_sum<LS>(cq);
+      xv = sys_sum<LS>(xv);
+      if (live_q) {
+        double* __restrict__ R = rec + q * M::R;
+        double* __restrict__ S = R + 4 + sd * M::SB;
+        if (sd == 0 && t == 0) {
+          R[0] = 1.0 / (double)nn;
+          R[1] = cq * A.wd;
+          R[2] = xv;
+          R[3] = rh[qs];
+        }
+        // block coordinates: [0, K) mlp, [K, 2K) gmf; the record holds x_mlp and W3g * x_gmf
+        S[ca] = ca < K ? y0 : w.W3[H2 + ca - K] * y0;
+        S[cb] = cb < K ? y1 : w.W3[H2 + cb - K] * y1;
+        if (t == 0) S[2 * K] = (double)(sd ? s_u[qs] : s_i[qs]);
+        if (x_out) {
+          x_out[q * D + M::ref_index(sd * Ds + ca)] = y0;
+          x_out[q * D + M::ref_index(sd * Ds + cb)] = y1;
+        }
+      } else if (q < Q && nn == 0) {
+        if (x_out) {
+          x_out[q * D + sd * Ds + ca] = NAN;
+          x_out[q * D + sd * Ds + cb] = NAN;
+        }
+        if (sd == 0 && t == 0) rec[q * M::R] = NAN;
+      } else if (q < Q && sd == 0 && t == 0) {      // coupled: the full-D solve finishes it
         const int slot = atomicAdd(coupled_out, 1);
         coupled_out[1 + slot] = (int32_t)q;
       }
-      continue;
     }
-    // H_b = (2/n) Gram_b + (wd + damping) I  (every NCF coordinate is decayed)
-#pragma unroll
-    for (int r = 0; r < N; ++r) col[r] *= s2n;
-#pragma unroll
-    for (int r = 0; r < N; ++r)
-      if (r == c) col[r] += A.wd + A.damping;
-    double y = live ? g[b * N + c] : 0.0;
-    double dinv_own = 0.0;
-    double* __restrict__ Pb = Pv + b * 34;           // column slots [0, 32), y_j at 32, dummy 33
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      Pb[c] = col[j];                                // A[c][j] (= col[j] by symmetry)
-      Pb[c == j ? 32 : 33] = y;                      // y_j is final: the forward solve rides along
-      wave_lds_sync();
-      const double dj = Pb[j];
-      double ij = __builtin_amdgcn_rcp(dj);
-      ij = fma(ij, fma(-dj, ij, 1.0), ij);
-      ij = fma(ij, fma(-dj, ij, 1.0), ij);
-      if (c == j) dinv_own = ij;
-      const double f = c > j ? col[j] * ij : 0.0;
-      const double yj = Pb[32];
-      y = fma(-f, yj, y);
-#pragma unroll
-      for (int r = 0; r < N; ++r)
-        if (r > j) col[r] = fma(-Pb[r], f, col[r]);
-      if (c > j) col[j] = f;
-      wave_lds_sync();
-    }
-    y *= dinv_own;
-#pragma unroll
-    for (int j = N - 1; j >= 0; --j) {               // L^T x = D^-1 y
-      const double lo = readlane_d(y, j), hi = readlane_d(y, 32 + j);
-      const double xj = b ? hi : lo;
-      if (c < j) y = fma(-col[j] * dinv_own, xj, y);
-    }
-    if (live) xs[b * N + c] = y;
-    __syncthreads();
-    solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, xs, w, rec + q * M::R, x_out);
+    STAMP(6);
   }
+#ifdef FIA_STAMPS
+  if (threadIdx.x == 0 && (blockIdx.x % 512) == 0)
+    printf("stamps blk %d iters %d: ids %lld prologue %lld loads %lld elim %lld back %lld epi %lld loop %lld\n",
+           (int)blockIdx.x, iters, st[1], st[2], st[3], st[4], st[5], st[6], st[0]);
+#endif
+#undef STAMP
 }
 
 // ------------------------------------------------------------------------------------
@@ -1300,6 +1529,11 @@ struct GramSides {
   const float* rating[2];
   const float* gbias;
   double* lres;
+  // fia_prepare_for (small k): only the entities marked here (users [0, U), items [U, U+I))
+  // get their Gram caches / per-position rows; nullptr = every entity
+  const uint8_t* mark;
+  int64_t moff[2];
+  __device__ bool skip(int sd, int32_t e) const { return mark && !mark[moff[sd] + e]; }
 };
 
 
@@ -1362,6 +1596,7 @@ __global__ __launch_bounds__(64) void k_resid_list_mf(GramSides GSd) {
   const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
   if (w >= GSd.n_items[sd]) return;
   const int32_t* __restrict__ items = GSd.items[sd];
+  if (GSd.skip(sd, items[4 * w])) return;
   resid_slice<M>(GSd, sd, items[4 * w], items[4 * w + 1], items[4 * w + 2], threadIdx.x);
 }
 
@@ -1381,6 +1616,7 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
   double* __restrict__ gram = GSd.gram[sd];
   double* __restrict__ part = GSd.part[sd];
   const int32_t e = items[4 * w], start = items[4 * w + 1], len = items[4 * w + 2], slot = items[4 * w + 3];
+  if (GSd.skip(sd, e)) return;
   const int lane = threadIdx.x;
   const int col = lane & 15, grp = lane >> 4;
   const int32_t* ids = other + ptr[e] + start;
@@ -1543,6 +1779,7 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
     }
     const int32_t* __restrict__ it = GSd.items[sd] + 4 * wi;
     const int32_t e = it[0], start = it[1], len = it[2], slot = it[3];
+    if (GSd.skip(sd, e)) continue;
     const int64_t lb = GSd.ptr[sd][e] + start;
     const int32_t* __restrict__ ids = GSd.other[sd] + lb;
     const float* __restrict__ rat = (sd ? rat1 : rat0) + lb;
@@ -1695,7 +1932,7 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
                                                      const double* __restrict__ part0, double* __restrict__ gram0,
                                                      int64_t n_comb1, const int32_t* __restrict__ comb1,
                                                      const double* __restrict__ part1, double* __restrict__ gram1,
-                                                     int GS, int GSP) {
+                                                     int GS, int GSP, const uint8_t* __restrict__ mark, int64_t moff1) {
   const int sd = (int64_t)blockIdx.x >= n_comb0 ? 1 : 0;
   const int64_t w = (int64_t)blockIdx.x - (sd ? n_comb0 : 0);
   if (w >= (sd ? n_comb1 : n_comb0)) return;
@@ -1703,6 +1940,7 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
   const double* __restrict__ part = sd ? part1 : part0;
   double* __restrict__ gram = sd ? gram1 : gram0;
   const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
+  if (mark && !mark[(sd ? moff1 : 0) + e]) return;
   // partials summed in slot order (deterministic), their loads issued 8 slots at a time
   // rather than one dependent round trip per slot
   for (int t = threadIdx.x; t < GS; t += 64) {
@@ -1732,7 +1970,8 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
 // chunk's descriptor, list entries and record words are loaded while the current
 // chunk's gathers are in flight, so each chunk waits on one round trip.
 // ------------------------------------------------------------------------------------
-// k_score_mf_run (MF k <= 16, the headline kernel): the per-query chunks of k_score_mf,
+// k_score_mf_run (MF k <= 16, opt-in via FIA_MF_SCORE=run; k_score_mf is the default headline
+// kernel): the per-query chunks of k_score_mf,
 // except that an item-side chunk is scored ONCE for a run of consecutive batch queries
 // with the same test item (<= kRunQB, runs cut at multiples of kRunQB): the run's first
 // query ("head") gathers the chunk's other-side rows once and scores every query of the
@@ -3048,14 +3287,14 @@ static int solve_mode() {
   return m;
 }
 
-// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): run | old
+// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): old (default) | run
 static const char* mf_score_mode() {
   static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "old";
   return m;
 }
 
 template <class M>
-hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
+hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
   constexpr int Ds = M::Ds, GS = Ds * (Ds + 1) / 2, K = M::K;
   const int64_t n_ent[2] = {c->p.U, c->p.I};
   for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gram[sd].reserve(sizeof(double) * (size_t)(n_ent[sd] * ((GS + 1) & ~1) + 1), s));
@@ -3096,6 +3335,9 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   }
   G.W3 = c->p.t[8];
   G.N = X.N;
+  G.mark = mark;
+  G.moff[0] = 0;
+  G.moff[1] = n_ent[0];
   if constexpr (M::ncf) {
     // per list position of each side: g_mlp (coordinate-major) and e, with the Grams
     const int64_t N = X.N;
@@ -3140,7 +3382,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s) {
   if (nc0 + nc1 > 0) {
     hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)(nc0 + nc1)), dim3(64), 0, s, nc0, X.gcomb[0].as<int32_t>(),
                        c->gpart[0].as<double>(), c->gram[0].as<double>(), nc1, X.gcomb[1].as<int32_t>(),
-                       c->gpart[1].as<double>(), c->gram[1].as<double>(), GS, GSP);
+                       c->gpart[1].as<double>(), c->gram[1].as<double>(), GS, GSP, mark, n_ent[0]);
     FIA_HIP_TRY(hipGetLastError());
   }
   return hipSuccess;
@@ -3167,8 +3409,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int qblock = use_mfma ? kMfmaQB : query_block<M>();
   // candidate slot sets per chunk: k_score_grouped writes one per pass
   constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
-  // MF k <= 16 per-query chunks: k_score_mf_run (A/B knob FIA_MF_SCORE=run|res|old), one
-  // candidate slot set per chunk
+  // MF k <= 16 per-query chunks: k_score_mf (default) or k_score_mf_run (A/B knob
+  // FIA_MF_SCORE=run), one candidate slot set per chunk
   const char* mfs = mf_score_mode();
   const bool runs = !M::ncf && M::K <= 16 && !grouped && !strcmp(mfs, "run");
   const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
@@ -3200,7 +3442,9 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       if constexpr (use_col_solve<M>()) {
         static const int64_t genv = getenv("FIA_SOLVE_GRID") ? atoll(getenv("FIA_SOLVE_GRID")) : 0;  // A/B knob
         const int64_t cap = genv > 0 ? genv : (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;
-        const int64_t g1 = Q < cap ? Q : cap;     // persistent: NCF weights staged once per block
+        constexpr int QW = 32 / M::K;             // queries per wave
+        const int64_t need = (Q + QW - 1) / QW;
+        const int64_t g1 = need < cap ? need : cap;   // persistent: NCF weights staged once per block
         hipLaunchKernelGGL(k_solve_col<M>, dim3((unsigned)g1), dim3(64), 0, s, A, Q, c->rec.as<double>(), x_out,
                            c->coupled.as<int32_t>());
       }
@@ -3265,7 +3509,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
                          c->cand_val.as<double>());
   } else {
-    // A/B knob FIA_MF_SCORE: run (default, k <= 16) | res | old (per-query residual dots)
+    // A/B knob FIA_MF_SCORE: old (default, k_score_mf) | run (opt-in item runs, k_score_mf_run)
     if constexpr (!M::ncf) {
       if constexpr (M::K <= 16) {
         if (runs) {
@@ -3338,12 +3582,73 @@ int model_num_params(int model, int k) {
 
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported) {
   unsupported = false;
-#define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_impl<T>(c, s);
+  c->subset = false;
+  c->small_subset = false;
+#define X(m, kk, T) if (c->p.model == m && c->p.k == kk) return prepare_impl<T>(c, s, nullptr);
   FIA_MODEL_CASES(X)
 #undef X
   if (big_supported(c->p.model, c->p.k)) return prepare_big(c, 0, nullptr, nullptr, s);
   unsupported = true;
   return hipSuccess;
+}
+
+// fia_prepare_for, small k: the queries' users and items are marked on the device (no host
+// round trip) and only their Gram caches (NCF: and per-position rows) are built; the cover
+// check of later fia_count_related calls reads the same marks
+__global__ void k_mark_small(int64_t Q, const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t U,
+                             int64_t I, uint8_t* __restrict__ mark) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = qu[q], i = qi[q];
+    if (u >= 0 && u < U && i >= 0 && i < I) {
+      mark[u] = 1;
+      mark[U + i] = 1;
+    }
+  }
+}
+
+__global__ void k_check_mark(int64_t Q, const int32_t* __restrict__ qu, const int32_t* __restrict__ qi, int64_t U,
+                             int64_t I, const uint8_t* __restrict__ mark, int32_t* __restrict__ flag) {
+  int bad = 0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < Q; q += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t u = qu[q], i = qi[q];
+    if (u >= 0 && u < U && i >= 0 && i < I) bad |= !mark[u] || !mark[U + i];
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+hipError_t prepare_model_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s,
+                             bool& unsupported) {
+  unsupported = false;
+  const int64_t U = c->p.U, I = c->p.I;
+  FIA_HIP_TRY(c->mark.reserve((size_t)(U + I), s));
+  FIA_HIP_TRY(hipMemsetAsync(c->mark.ptr, 0, (size_t)(U + I), s));
+  if (Q > 0) {
+    const int64_t gq = (Q + 255) / 256;
+    hipLaunchKernelGGL(k_mark_small, dim3((unsigned)(gq < 4096 ? gq : 4096)), dim3(256), 0, s, Q, qu, qi, U, I,
+                       c->mark.as<uint8_t>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  c->subset = false;
+  c->small_subset = false;
+#define X(m, kk, T)                                                     \
+  if (c->p.model == m && c->p.k == kk) {                                \
+    FIA_HIP_TRY(prepare_impl<T>(c, s, c->mark.as<uint8_t>()));          \
+    c->small_subset = true;                                             \
+    return hipSuccess;                                                  \
+  }
+  FIA_MODEL_CASES(X)
+#undef X
+  unsupported = true;
+  return hipSuccess;
+}
+
+hipError_t check_cover_small(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag,
+                             hipStream_t s) {
+  if (!c->small_subset || Q <= 0) return hipSuccess;
+  const int64_t gq = (Q + 255) / 256;
+  hipLaunchKernelGGL(k_check_mark, dim3((unsigned)(gq < 4096 ? gq : 4096)), dim3(256), 0, s, Q, qu, qi, c->p.U, c->p.I,
+                     c->mark.as<uint8_t>(), flag);
+  return hipGetLastError();
 }
 
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,

@@ -93,6 +93,8 @@ class Context(object):
             raise FIAError("fia_create(%d) failed: %s" % (device, _ERR.get(rc, rc)))
         self.h = h
         self._keep = []
+        self._mask = 0
+        self._carry = None      # phase sums drained by profiled_call on the caller's behalf
 
     def close(self):
         if getattr(self, "h", None):
@@ -171,10 +173,39 @@ class Context(object):
         mask = 0
         if on:
             mask = 0x1f if phases is None else sum(1 << PHASES.index(p) for p in phases)
-        self._check(self.lib.fia_set_profiling(self.h, mask), "fia_set_profiling")
+        self._set_mask(mask)
 
-    def profile_read(self):
+    def _set_mask(self, mask):
+        self._check(self.lib.fia_set_profiling(self.h, mask), "fia_set_profiling")
+        self._mask = mask
+
+    def _drain(self):
         ms = (ctypes.c_double * FIA_NUM_PHASES)()
         cnt = (ctypes.c_int64 * FIA_NUM_PHASES)()
         self._check(self.lib.fia_profile_read(self.h, ms, cnt), "fia_profile_read")
         return {PHASES[p]: (ms[p], cnt[p]) for p in range(FIA_NUM_PHASES)}
+
+    def profile_read(self):
+        """Per-phase (ms sum, count) recorded since the last read (synchronises the events)."""
+        out = self._drain()
+        if self._carry is not None:
+            out = {p: (out[p][0] + self._carry[p][0], out[p][1] + self._carry[p][1]) for p in PHASES}
+            self._carry = None
+        return out
+
+    def profiled_call(self, fn):
+        """Run fn() with every phase recorded and return (fn's result, its phase sums).  The
+        caller's profiling mask and the sums it has accumulated but not yet read are kept
+        (the RQ2 timers of a single query, GenericNeuralNet.get_influence_on_test_loss)."""
+        before = self._drain()
+        mask = self._mask
+        self._set_mask(0x1f)
+        try:
+            res = fn()
+        finally:
+            self._set_mask(mask)
+        mine = self._drain()
+        if self._carry is not None:
+            before = {p: (before[p][0] + self._carry[p][0], before[p][1] + self._carry[p][1]) for p in PHASES}
+        self._carry = before
+        return res, mine

@@ -407,13 +407,9 @@ class GenericNeuralNet(object):
         # the three RQ2 stage timers (mf:224-250) come from the library's HIP-event phases of
         # this one call: inverse HVP = related lists + Hessian assembly + solve, multiplying =
         # per-rating scoring (+ the fused top-K)
-        self.ctx.profile_read()
-        self.ctx.set_profiling(True)
-        try:
-            res = self.get_influence_batch(test_indices, K=0, full=True, return_x=True)
-        finally:
-            self.ctx.set_profiling(False)
-        phases = self.ctx.profile_read()
+        # (the caller's own profiling mask and unread sums are kept: Context.profiled_call)
+        res, phases = self.ctx.profiled_call(
+            lambda: self.get_influence_batch(test_indices, K=0, full=True, return_x=True))
         self.train_indices_of_test_case = res["rel_idx"]
         x = res["x"][0]
         self.num_params = x.size

@@ -93,13 +93,15 @@ int fia_build_index(fia_ctx* ctx, int64_t n_train, int64_t num_users, int64_t nu
  * and again whenever the parameter VALUES change. */
 int fia_prepare(fia_ctx* ctx, void* stream);
 
-/* Like fia_prepare, but the per-entity caches of the large-k models (MF k >= 128,
- * NCF k >= 64) are built only for the users and items referenced by the Q queries
- * (q_user / q_item, device int32): one GPU's query shard needs its own users and the
- * items they rated, not the whole table (20M ratings, NCF k=256: 1 MB per entity).
- * Later fia_count_related calls (with total_out) reject queries outside that set
- * (FIA_ERR_STATE).  Small-k models build every cache, exactly as fia_prepare.
- * Synchronises `stream` (the cache size is decided on the host). */
+/* Like fia_prepare, but the per-entity caches are built only for the users and items
+ * referenced by the Q queries (q_user / q_item, device int32): one GPU's query shard needs
+ * its own users and items, not the whole table.  Later fia_count_related calls (with
+ * total_out) reject queries outside that set (FIA_ERR_STATE).
+ *   large k (MF k >= 128, NCF k >= 64): compacted caches (20M ratings, NCF k=256: 1 MB per
+ *     entity); synchronises `stream` (the cache size is decided on the host);
+ *   small k: the entities are marked on the device and only their caches are computed (the
+ *     layout stays dense); stream-ordered, no synchronisation.
+ * Results for covered queries are bitwise identical to those after fia_prepare. */
 int fia_prepare_for(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const int32_t* q_item, void* stream);
 
 /* offsets[q] = sum_{q'<q} n_q', offsets[Q] = total, with n_q = |R_u| + |C_i|

@@ -128,3 +128,41 @@ def test_lissa_is_refused_not_ignored():
         m.get_influence_on_test_loss([0], np.arange(3), approx_type="lissa")
     with pytest.raises(ValueError):
         m.get_influence_on_test_loss([0], np.arange(3), approx_type="newton")
+
+
+def test_profiled_call_keeps_caller_profiling_state():
+    """get_influence_on_test_loss times its own call (RQ2 timers) through
+    Context.profiled_call: the caller's phase mask is restored and the sums it had
+    accumulated but not read are still returned by its next profile_read."""
+    from influence import _lib
+
+    class FakeLib:
+        def __init__(self):
+            self.mask, self.pending = 0, [0.0] * _lib.FIA_NUM_PHASES
+
+        def fia_set_profiling(self, h, mask):
+            self.mask = mask
+            return 0
+
+        def run(self, ms):                      # a library call: records the enabled phases
+            for p in range(_lib.FIA_NUM_PHASES):
+                if self.mask >> p & 1:
+                    self.pending[p] += ms
+
+        def fia_profile_read(self, h, ms, cnt):
+            for p in range(_lib.FIA_NUM_PHASES):
+                ms[p], cnt[p] = self.pending[p], int(self.pending[p] > 0)
+            self.pending = [0.0] * _lib.FIA_NUM_PHASES
+            return 0
+
+    ctx = object.__new__(_lib.Context)
+    ctx.lib, ctx.h, ctx._mask, ctx._carry = FakeLib(), None, 0, None
+    ctx.set_profiling(True, phases=("score",))
+    ctx.lib.run(2.0)                            # the caller's own measurement, not yet read
+    res, mine = ctx.profiled_call(lambda: ctx.lib.run(5.0) or "r")
+    assert res == "r"
+    assert mine["score"][0] == 5.0 and mine["solve"][0] == 5.0     # every phase during the call
+    assert ctx._mask == 1 << _lib.PHASES.index("score")             # caller's mask restored
+    ctx.lib.run(1.0)
+    after = ctx.profile_read()
+    assert after["score"][0] == 3.0 and after["solve"][0] == 0.0    # 2 (before) + 1 (after)

@@ -304,10 +304,12 @@ def test_large_k_matches_oracle(model, k, tmp_path):
         assert (infl[rel == row] == infl[rel == row][0]).all()
 
 
-@pytest.mark.parametrize("model,k", [("MF", 128), ("NCF", 64)])
+@pytest.mark.parametrize("model,k", [("MF", 128), ("NCF", 64), ("MF", 16), ("MF", 64), ("NCF", 16)])
 def test_prepare_for_subset(model, k, tmp_path):
     """fia_prepare_for: caches for only the queried users/items give the same
-    results as the full prepare, and a query outside the set is rejected."""
+    results as the full prepare (bitwise), and a query outside the set is rejected
+    until the next full prepare.  Large k: compacted slot caches; small k: dense caches
+    of the marked entities only."""
     from influence._lib import FIAError
     rng = np.random.default_rng(5)
     U, I, N = 300, 40, 4000
@@ -331,6 +333,10 @@ def test_prepare_for_subset(model, k, tmp_path):
         assert np.array_equal(part["x"][j], full["x"][q])
     with pytest.raises(FIAError):
         m.get_influence_batch([11], K=1)
+    m.ctx.prepare()                              # every cache again: the query is answered
+    again = m.get_influence_batch([11], K=2)
+    b, e = full["offsets"][11], full["offsets"][12]
+    assert np.array_equal(again["influence"], full["influence"][b:e])
 
 
 @pytest.mark.parametrize("model,k", [("MF", 16), ("NCF", 8), ("MF", 32), ("MF", 64)])

@@ -107,21 +107,26 @@ def test_two_ranks_on_one_gpu_equal_single_process(model, k):
     assert res[0][1] == res[1][0] and res[1][1] == qu.size
 
 
-@pytest.mark.parametrize("scaling", ["weak", "strong"])
+@pytest.mark.parametrize("scaling", ["default", "weak", "strong"])
 def test_bench_two_ranks(scaling, tmp_path):
     """bench.py --gpus 2 (self-launched under torch.distributed.run; both ranks on cuda:0, so
-    gloo carries the top-K exchange): one JSON line with n_gpus 2 and the node's total."""
+    gloo carries the top-K exchange): one JSON line with n_gpus 2 and the node's total.  The
+    default is strong scaling of the real ml-1m-ex test set; weak scaling is opt-in and labels
+    its synthetic re-paired queries in config.workload."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-           "--scaling", scaling, "--no-cpu-baseline"]
+           "--no-cpu-baseline"] + ([] if scaling == "default" else ["--scaling", scaling])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["scaling"] == scaling and out["value"] > 0
+    want = "strong" if scaling == "default" else scaling
+    assert out["n_gpus"] == 2 and out["scaling"] == want and out["value"] > 0
     sizes = out["config"]["queries_per_rank"]
-    if scaling == "weak":
+    if want == "weak":
         assert sizes == [12074, 12074]
+        assert "synthetic re-paired" in out["config"]["workload"]
     else:
         assert sum(sizes) == 12074 and min(sizes) > 0
+        assert "re-paired" not in out["config"]["workload"]
     assert out["config"]["node_queries_per_step"] == sum(sizes)
