@@ -303,9 +303,10 @@ int fia_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, con
   })
 }
 
-int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                    int64_t total_rel, int32_t* rel_idx, double* influence, double* x_out, int K,
-                    int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream) {
+static int query_batch_common(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                              int64_t total_rel, int32_t* rel_idx, double* influence, double* x_out, int K,
+                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream,
+                              const double* x_in) {
   if (!c) return FIA_ERR_INVALID;
   FIA_GUARDED(c, {
     if (!c->p.valid || !c->idx.valid) return fail(c, FIA_ERR_STATE, "params/index missing");
@@ -321,11 +322,28 @@ int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
     const int64_t max_chunks = 2 * Q + total_rel / fia::kChunk + 1;
     bool unsup = false;
     hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,
-                                    topk_idx, topk_val, as_stream(stream), unsup);
-    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
+                                    topk_idx, topk_val, as_stream(stream), unsup, x_in);
+    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, x_in ? "scoring from a given x is built for the small-k models"
+                                                         : "model/k not supported");
     if (e != hipSuccess) return hip_fail(c, e, "fia_query_batch");
     return FIA_OK;
   })
+}
+
+int fia_query_batch(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                    int64_t total_rel, int32_t* rel_idx, double* influence, double* x_out, int K,
+                    int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream) {
+  return query_batch_common(c, Q, qu, qi, offsets, total_rel, rel_idx, influence, x_out, K, topk_pos, topk_idx,
+                            topk_val, stream, nullptr);
+}
+
+int fia_query_batch_x(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
+                      int64_t total_rel, const double* x_in, int32_t* rel_idx, double* influence, int K,
+                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream) {
+  if (!c) return FIA_ERR_INVALID;
+  if (Q > 0 && !x_in) return fail(c, FIA_ERR_INVALID, "null x_in");
+  return query_batch_common(c, Q, qu, qi, offsets, total_rel, rel_idx, influence, nullptr, K, topk_pos, topk_idx,
+                            topk_val, stream, x_in);
 }
 
 int fia_set_profiling(fia_ctx* c, int phase_mask) {

@@ -259,7 +259,8 @@ hipError_t check_cover_small(fia_ctx* c, int64_t Q, const int32_t* qu, const int
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                        int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                        int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
-                       bool& unsupported);
+                       bool& unsupported,
+                       const double* x_in = nullptr);
 int model_num_params(int model, int k);
 bool model_supported(int model, int k);
 

@@ -344,7 +344,7 @@ __global__ void k_group_fill(const int32_t* __restrict__ qu, const int32_t* __re
 // count array.  tstate: two arrays of tile words (queries, work items); the last tile to
 // finish re-zeroes them and the two counters.
 __global__ __launch_bounds__(kScanThreads) void k_group_scan(
-    const unsigned long long* __restrict__ gcnt, const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr,
+    unsigned long long* __restrict__ gcnt, const int64_t* __restrict__ uptr, const int64_t* __restrict__ iptr,
     int64_t U, int64_t I, int qb, int cpi, int64_t* __restrict__ gstart, int64_t* __restrict__ wstart,
     unsigned long long* __restrict__ tstate, unsigned int* __restrict__ tctr) {
   __shared__ int s_tile;
@@ -360,6 +360,9 @@ __global__ __launch_bounds__(kScanThreads) void k_group_scan(
   int64_t a = 0, b = 0;
   if (t < nE) {
     a = (int64_t)gcnt[t];
+    // this thread is the count's only reader here (k_item_fill takes it from gstart): leave
+    // it zero for the next batch's k_group_count -- no memset on the query path
+    if (a > 0) gcnt[t] = 0;
     if (a > 0) {
       const int64_t deg = t < U ? uptr[t + 1] - uptr[t] : iptr[t - U + 1] - iptr[t - U];
       b = ((deg + kChunk * cpi - 1) / (kChunk * cpi)) * ((a + qb - 1) / qb);
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(kScanThreads) void k_group_scan(
 
 // thread per work item (grid-stride up to wstart[nE]): its entity by binary search over
 // wstart, then {entity, chunk of the entity's list, block of the entity's query group}
-__global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned long long* __restrict__ gcnt,
+__global__ void k_item_fill(const int64_t* __restrict__ wstart, const int64_t* __restrict__ gstart,
                             int64_t nE, int32_t* __restrict__ witems, int qb) {
   const int64_t total = wstart[nE];
   for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < total;
@@ -417,7 +420,7 @@ __global__ void k_item_fill(const int64_t* __restrict__ wstart, const unsigned l
       if (wstart[mid] <= w) lo = mid; else hi = mid - 1;
     }
     const int64_t b = wstart[lo];
-    const int64_t nqb = ((int64_t)gcnt[lo] + qb - 1) / qb;
+    const int64_t nqb = (gstart[lo + 1] - gstart[lo] + qb - 1) / qb;     // the entity's query count
     witems[3 * w] = (int32_t)lo;
     witems[3 * w + 1] = (int32_t)((w - b) / nqb);    // chunk of the entity's list
     witems[3 * w + 2] = (int32_t)((w - b) % nqb);    // block of the entity's query group
@@ -656,7 +659,11 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                         int64_t max_items, int qb, hipStream_t s, int cpi) {
   const int64_t U = c->idx.U, I = c->idx.I, nE = U + I;
   const int64_t ntiles = (nE + 1 + kScanTile - 1) / kScanTile;
-  FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
+  // per-entity query counts: zero at allocation, left zero by k_group_scan
+  if (c->gcnt.bytes < sizeof(int64_t) * (size_t)(nE + 1) || !c->gcnt.ptr) {
+    FIA_HIP_TRY(c->gcnt.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
+    FIA_HIP_TRY(hipMemsetAsync(c->gcnt.ptr, 0, c->gcnt.bytes, s));
+  }
   FIA_HIP_TRY(c->gstart.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
   FIA_HIP_TRY(c->wstart.reserve(sizeof(int64_t) * (size_t)(nE + 1), s));
   FIA_HIP_TRY(c->grank.reserve(sizeof(int32_t) * (size_t)(2 * Q + 1), s));
@@ -671,7 +678,6 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
   }
   const int64_t* uptr = c->idx.side[0].ptr.as<int64_t>();
   const int64_t* iptr = c->idx.side[1].ptr.as<int64_t>();
-  FIA_HIP_TRY(hipMemsetAsync(c->gcnt.ptr, 0, sizeof(int64_t) * (size_t)(nE + 1), s));
   if (Q > 0) {
     hipLaunchKernelGGL(k_group_count, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, qu, qi, Q, uptr, iptr, U, I,
                        offsets, c->coff.as<int64_t>(), c->gcnt.as<unsigned long long>(), c->grank.as<int32_t>(),
@@ -689,7 +695,7 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
     FIA_HIP_TRY(hipGetLastError());
   }
   hipLaunchKernelGGL(k_item_fill, dim3(grid_for(max_items, 256, 16384)), dim3(256), 0, s, c->wstart.as<int64_t>(),
-                     c->gcnt.as<unsigned long long>(), nE, c->witems.as<int32_t>(), qb);
+                     c->gstart.as<int64_t>(), nE, c->witems.as<int32_t>(), qb);
   return hipGetLastError();
 }
 

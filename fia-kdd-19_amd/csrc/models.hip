@@ -694,6 +694,44 @@ __global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(
   }   // work loop
 }
 
+// Scoring records from a GIVEN inverse HVP (fia_query_batch_x: the reference's cached
+// <model>-cg-normal_loss-test-[t].npz when force_refresh is False, mf:210-214): one wave per
+// query, theta_t / v / r-hat by the solve prologue, x = x_in (reference theta order)
+// instead of a solve, then the solve epilogue's record.
+template <class M>
+__global__ __launch_bounds__(kSolveThreads) void k_record_x(QueryArgs A, int64_t Q, const double* __restrict__ x_in,
+                                                            double* __restrict__ rec, double* __restrict__ x_out) {
+  constexpr int K = M::K, D = M::D;
+  __shared__ double v[D], g[D], th[D];
+  __shared__ double sh[4 * K + 8];
+  __shared__ NCFWeights<M::ncf ? K : 2> w;
+  __shared__ double sW1[M::ncf ? 2 * K * K : 1];
+  __shared__ double sb1[M::ncf ? K : 1];
+  if constexpr (M::ncf) {
+    load_ncf_weights<K>(w, A.t[6], A.t[7], A.t[8]);
+    for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
+    for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
+  }
+  for (int64_t q = blockIdx.x; q < Q; q += gridDim.x) {
+    __syncthreads();
+    const int lane = threadIdx.x;
+    const int32_t u = A.qu[q], i = A.qi[q];
+    double* R = rec + q * M::R;
+    const bool ok_id = (u >= 0 && u < A.U && i >= 0 && i < A.I);
+    const int64_t n = ok_id ? (A.ptr[0][u + 1] - A.ptr[0][u]) + (A.ptr[1][i + 1] - A.ptr[1][i]) : 0;
+    if (n == 0) {
+      if (x_out)
+        for (int a = lane; a < D; a += kSolveThreads) x_out[q * D + a] = NAN;
+      if (lane == 0) R[0] = NAN;
+      continue;
+    }
+    const double rhat_ui = solve_prologue<M, kSolveThreads>(A, u, i, th, g, sh, w, sW1, sb1);
+    for (int a = lane; a < D; a += kSolveThreads) v[a] = x_in[q * D + M::ref_index(a)];
+    __syncthreads();
+    solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, v, w, R, x_out);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Side-system solve on 16x16 tiles (NCF, MF k >= 32): one wave per (query, side) system.
 //
@@ -2811,6 +2849,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     double* outp[4];
     int32_t* relp[4];
     int32_t dupo[4], cpos[4];
+    int dl[4] = {0, 0, 0, 0};         // misalignment of each query row's output run (elements)
     int64_t cslot[4];
     bool qv[4];
     if constexpr (SETUP >= 1) {
@@ -2836,8 +2875,16 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
         const int64_t ob = (sd ? q01.y : q01.x) + p0 + cn;
         cslot[r] = (sd ? q23.y : q23.x) + (int64_t)cg * CPI;
         cpos[r] = (int32_t)(p0 + sd * (q01.y - q01.x));
+#ifndef FIA_MFMA_NO_ROT
+        // aligned stores: the run starts dl elements into a 16-element (128-B influence,
+        // 64-B train-row) segment; lane cn stores segment element cn
+        dl[r] = (int)((ob - cn) & 15);
+        outp[r] = influence + (ob - dl[r]);
+        relp[r] = rel_idx + (ob - dl[r]);
+#else
         outp[r] = influence + ob;
         relp[r] = rel_idx + ob;
+#endif
       }
     } else {
 #pragma unroll
@@ -2855,8 +2902,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
         const int64_t ob = qb[sd] + p0 + cn;
         cslot[r] = qb[2 + sd] + (int64_t)cg * CPI;           // candidate slot of the item's first chunk
         cpos[r] = (int32_t)(p0 + (sd ? qb[1] - qb[0] : 0));  // |R_u| precedes item-side positions
+#ifndef FIA_MFMA_NO_ROT
+        dl[r] = (int)((ob - cn) & 15);
+        outp[r] = influence + (ob - dl[r]);
+        relp[r] = rel_idx + (ob - dl[r]);
+#else
         outp[r] = influence + ob;
         relp[r] = rel_idx + ob;
+#endif
       }
     }
     long long bk[4];
@@ -2864,6 +2917,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     double bv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) { bk[r] = -2; bp[r] = 0x7fffffff; bv[r] = 0.0; }
+    double prv[4] = {0.0, 0.0, 0.0, 0.0};     // previous tile's rotated values (aligned stores)
+    int32_t prw[4] = {0, 0, 0, 0};
     const int ntl = (len + 15) / 16;
     // software pipeline over the tiles, ring of three slots: the list entries of tile t + 2
     // and the gathered rows of tile t + 1 are in flight while tile t is scored.  Positions
@@ -2935,6 +2990,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
       const double dself = __shfl(acc[3], 48 + cn);
       const double en = ((dself + bself) + (double)sbo[k3]) + gbias - y;
       const bool dup = pv && (o == dupo[0] || o == dupo[1] || o == dupo[2] || o == dupo[3]);
+      double val[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) val[r] = fma(en * al[r], acc[r] + xb[r], be[r]);
       if (__builtin_expect(__ballot(dup) != 0, 0)) {
         // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
 #pragma unroll
@@ -2942,26 +3000,38 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
           if (!(pv && qv[r] && o == dupo[r])) continue;
           const int32_t q = gq[gb + kk + 4 * r];
           const double* __restrict__ R = rec + (int64_t)q * M::R;
-          const double infl = fma((R[3] - y) * al[r], R[2], be[r]);
-          if (FULL || influence) st_out(infl, outp[r] + 16 * t);
-          if (FULL || rel_idx) st_out(w, relp[r] + 16 * t);
-          const long long key = topk_ikey(infl);
-          if (key > bk[r]) { bk[r] = key; bp[r] = p; bv[r] = infl; }
+          val[r] = fma((R[3] - y) * al[r], R[2], be[r]);
         }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool ok = pv && qv[r] && o != dupo[r];
-        const double infl = fma(en * al[r], acc[r] + xb[r], be[r]);
-        if (ok) {
-          if (FULL || influence) st_out(infl, outp[r] + 16 * t);
-          if (FULL || rel_idx) st_out(w, relp[r] + 16 * t);
-        }
-        const long long key = ok ? topk_ikey(infl) : -2ll;
+        const bool ok = pv && qv[r];
+        const long long key = ok ? topk_ikey(val[r]) : -2ll;
         const bool take = key > bk[r];
         bk[r] = take ? key : bk[r];
         bp[r] = take ? p : bp[r];
-        bv[r] = take ? infl : bv[r];
+        bv[r] = take ? val[r] : bv[r];
+#ifndef FIA_MFMA_NO_ROT
+        // rotate the row by its misalignment dl: lane cn takes element (cn - dl) & 15 -- of
+        // this tile (cn >= dl) or, already rotated, of the previous tile (cn < dl) -- so each
+        // store is one aligned 16-element segment (whole lines: no line written twice)
+        const int srcl = ((cn - dl[r]) & 15) + 16 * kk;
+        const double rv = __shfl(val[r], srcl);
+        const int32_t rw = __shfl(w, srcl);
+        const bool cur = cn >= dl[r];
+        const int idx = 16 * t + cn - dl[r];          // element of the run this lane stores
+        if (qv[r] && (cur ? idx < len : t > 0)) {
+          if (FULL || influence) st_out(cur ? rv : prv[r], outp[r] + 16 * t + cn);
+          if (FULL || rel_idx) st_out(cur ? rw : prw[r], relp[r] + 16 * t + cn);
+        }
+        prv[r] = rv;
+        prw[r] = rw;
+#else
+        if (ok) {
+          if (FULL || influence) st_out(val[r], outp[r] + 16 * t);
+          if (FULL || rel_idx) st_out(w, relp[r] + 16 * t);
+        }
+#endif
       }
       if (t % TPC == TPC - 1 || t == ntl - 1) emit(t / TPC);
     };
@@ -2981,6 +3051,17 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
       gather(0);
       tile(t + 2, 2);
     }
+#ifndef FIA_MFMA_NO_ROT
+    // the run's tail: the last tile's elements past the last aligned segment
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int idx = 16 * ntl + cn - dl[r];
+      if (qv[r] && cn < dl[r] && idx < len) {
+        if (FULL || influence) st_out(prv[r], outp[r] + 16 * ntl + cn);
+        if (FULL || rel_idx) st_out(prw[r], relp[r] + 16 * ntl + cn);
+      }
+    }
+#endif
   }
 }
 
@@ -3391,7 +3472,8 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
 template <class M>
 hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                       int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
-                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
+                      const double* x_in) {
   // Auto schedule (measured on MI355X, profiles/): entity-shared scoring wins whenever
   // the per-rating work is larger than a 64-B gather (k >= 32) -- 20M MF k=64 855 vs
   // 429 k q/s; for MF k <= 16 the group build costs more than the shared gathers save
@@ -3431,8 +3513,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? cpi_used : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
+  if (x_in && Q > 0) {
+    // a given inverse HVP: records straight from it, no solve (fia_query_batch_x)
+    const int64_t g1 = Q < 8192 ? Q : 8192;
+    hipLaunchKernelGGL(k_record_x<M>, dim3((unsigned)g1), dim3(kSolveThreads), 0, s, A, Q, x_in, c->rec.as<double>(),
+                       x_out);
+    FIA_HIP_TRY(hipGetLastError());
+  }
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
-  if (Q > 0) {
+  if (Q > 0 && !x_in) {
     static const bool tps_on = !getenv("FIA_NO_TPS");   // A/B knob: wave-per-query solve instead
     if (use_tps<M>() && tps_on) {
       if constexpr (use_tps<M>())
@@ -3653,14 +3742,19 @@ hipError_t check_cover_small(fia_ctx* c, int64_t Q, const int32_t* qu, const int
 
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                        int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
-                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s, bool& unsupported) {
+                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s, bool& unsupported,
+                       const double* x_in) {
   unsupported = false;
 #define X(m, kk, T)                                                                                        \
   if (c->p.model == m && c->p.k == kk)                                                                     \
     return query_impl<T>(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos, topk_idx, \
-                         topk_val, s);
+                         topk_val, s, x_in);
   FIA_MODEL_CASES(X)
 #undef X
+  if (x_in) {                          // large k: scoring from a given x is not built
+    unsupported = true;
+    return hipSuccess;
+  }
   if (big_supported(c->p.model, c->p.k))
     return query_big(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos, topk_idx, topk_val,
                      s);

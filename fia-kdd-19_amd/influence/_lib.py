@@ -37,6 +37,7 @@ SIGNATURES = {
     "fia_count_related": (ctypes.c_int, [_P, _I64, _P, _P, _P, ctypes.POINTER(_I64), _P]),
     "fia_related": (ctypes.c_int, [_P, _I64, _P, _P, _P, _P, _P]),
     "fia_query_batch": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P]),
+    "fia_query_batch_x": (ctypes.c_int, [_P, _I64, _P, _P, _P, _I64, _P, _P, _P, ctypes.c_int, _P, _P, _P, _P]),
     "fia_num_params": (ctypes.c_int, [_P]),
     "fia_set_profiling": (ctypes.c_int, [_P, ctypes.c_int]),
     "fia_profile_read": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64)]),
@@ -166,6 +167,19 @@ class Context(object):
                                       _ptr(rel_idx), _ptr(influence), _ptr(x), int(K), _ptr(topk_pos),
                                       _ptr(topk_idx), _ptr(topk_val), _stream())
         self._check(rc, "fia_query_batch")
+
+    def query_batch_x(self, qu, qi, offsets, total, x_in, rel_idx=None, influence=None, K=0,
+                      topk_pos=None, topk_idx=None, topk_val=None):
+        """fia_query_batch with the given inverse HVPs x_in (float64 cuda tensor [Q * D],
+        reference theta order) instead of the solve."""
+        import torch
+        self._need_int32(rel_idx, "rel_idx")
+        if x_in.dtype != torch.float64 or not x_in.is_contiguous():
+            raise TypeError("x_in must be a contiguous torch.float64 tensor")
+        rc = self.lib.fia_query_batch_x(self.h, qu.numel(), _ptr(qu), _ptr(qi), _ptr(offsets), int(total),
+                                        _ptr(x_in), _ptr(rel_idx), _ptr(influence), int(K), _ptr(topk_pos),
+                                        _ptr(topk_idx), _ptr(topk_val), _stream())
+        self._check(rc, "fia_query_batch_x")
 
     # ---- profiling ----
     def set_profiling(self, on, phases=None):

@@ -341,9 +341,11 @@ class GenericNeuralNet(object):
         u, i = self._test_pair(test_index[0])
         return self._theta_blocks(u, i)
 
-    def get_influence_batch(self, test_indices, K=1, full=True, return_x=True):
+    def get_influence_batch(self, test_indices, K=1, full=True, return_x=True, inverse_hvp=None):
         """Batched FIA over many test ratings (one fia_query_batch call).
 
+        inverse_hvp (optional, float64 [Q, D] in the reference theta order): score with these
+        inverse HVPs instead of solving (fia_query_batch_x; returned as x).
         Returns dict(offsets, rel_idx, influence, x, topk_pos, topk_idx, topk_val) as numpy
         arrays; influence[offsets[q]:offsets[q+1]] is get_influence_on_test_loss([t_q], ...)."""
         import torch
@@ -354,11 +356,18 @@ class GenericNeuralNet(object):
         D = self.ctx.num_params()
         rel = torch.empty(max(total, 1), dtype=torch.int32, device=dev) if full else None
         infl = torch.empty(max(total, 1), dtype=torch.float64, device=dev) if full else None
-        x = torch.empty(max(Q * D, 1), dtype=torch.float64, device=dev) if return_x else None
         tp = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev) if K else None
         ti = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev) if K else None
         tv = torch.empty(max(Q * K, 1), dtype=torch.float64, device=dev) if K else None
-        self.ctx.query_batch(qu, qi, offsets, total, rel, infl, x, K, tp, ti, tv)
+        if inverse_hvp is not None:
+            xin = np.ascontiguousarray(np.asarray(inverse_hvp, np.float64).reshape(-1))
+            if xin.size != Q * D:
+                raise ValueError("inverse_hvp must hold %d x %d values" % (Q, D))
+            x = torch.from_numpy(xin).to(dev)
+            self.ctx.query_batch_x(qu, qi, offsets, total, x, rel, infl, K, tp, ti, tv)
+        else:
+            x = torch.empty(max(Q * D, 1), dtype=torch.float64, device=dev) if return_x else None
+            self.ctx.query_batch(qu, qi, offsets, total, rel, infl, x, K, tp, ti, tv)
         out = dict(offsets=offsets.cpu().numpy())
         if full:
             out["rel_idx"] = rel[:total].cpu().numpy().astype(np.int64)
@@ -407,18 +416,26 @@ class GenericNeuralNet(object):
         # the three RQ2 stage timers (mf:224-250) come from the library's HIP-event phases of
         # this one call: inverse HVP = related lists + Hessian assembly + solve, multiplying =
         # per-rating scoring (+ the fused top-K)
+        if test_description is None:
+            test_description = test_indices
+        fname = os.path.join(self.train_dir, "%s-%s-%s-test-%s.npz" % (
+            self.model_name, approx_type, loss_type, test_description))
+        # the reference's cached inverse HVP (mf:210-214): with force_refresh False and the
+        # file present, its vector replaces the solve (scored on the GPU, fia_query_batch_x)
+        cached = None
+        if not force_refresh and os.path.exists(fname):
+            with np.load(fname, allow_pickle=False) as z:
+                cached = np.asarray(z["inverse_hvp"], np.float64).reshape(1, -1)
+            if self.verbose:
+                print("Loaded inverse HVP from %s" % fname)
         # (the caller's own profiling mask and unread sums are kept: Context.profiled_call)
         res, phases = self.ctx.profiled_call(
-            lambda: self.get_influence_batch(test_indices, K=0, full=True, return_x=True))
+            lambda: self.get_influence_batch(test_indices, K=0, full=True, return_x=True, inverse_hvp=cached))
         self.train_indices_of_test_case = res["rel_idx"]
         x = res["x"][0]
         self.num_params = x.size
         self.inverse_hvp = self._split_theta(x)
-        if test_description is None:
-            test_description = test_indices
-        if self.save_inverse_hvp:
-            fname = os.path.join(self.train_dir, "%s-%s-%s-test-%s.npz" % (
-                self.model_name, approx_type, loss_type, test_description))
+        if self.save_inverse_hvp and cached is None:
             np.savez(fname, inverse_hvp=x)
         self.last_timing = rq2_timing(phases, res["influence"].size, time.time() - t0,
                                       log=print if self.verbose else None)

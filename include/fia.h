@@ -136,6 +136,17 @@ int fia_query_batch(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, co
                     int32_t* rel_idx, double* influence, double* x_out,
                     int K, int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream);
 
+/* fia_query_batch with a GIVEN inverse HVP instead of the solve: x_in (device double[Q * D],
+ * the reference theta order, as fia_query_batch's x_out) replaces H_t^-1 v; the related sets,
+ * influence and top-K follow from it exactly as in fia_query_batch.  Replaces the reference's
+ * cached-inverse-HVP branch of get_influence_on_test_loss (force_refresh=False and an existing
+ * <model>-cg-normal_loss-test-[t].npz, matrix_factorization.py:210-214).  Small-k models only
+ * (MF k <= 64, NCF k <= 32); large k returns FIA_ERR_UNSUPPORTED. */
+int fia_query_batch_x(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const int32_t* q_item,
+                      const int64_t* offsets, int64_t total_rel, const double* x_in,
+                      int32_t* rel_idx, double* influence,
+                      int K, int64_t* topk_pos, int64_t* topk_idx, double* topk_val, void* stream);
+
 /* Number of restricted parameters D of the registered model (0 if none). */
 int fia_num_params(const fia_ctx* ctx);
 

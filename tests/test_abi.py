@@ -39,6 +39,7 @@ def test_host_only_entry_points(libfia_path):
     assert lib.fia_num_params(None) == 0
     assert lib.fia_set_params(None, 0, 16, 1, 1, None, 0, 0.0, 0.0) == 1
     assert lib.fia_query_batch(None, 0, None, None, None, 0, None, None, None, 0, None, None, None, None) == 1
+    assert lib.fia_query_batch_x(None, 0, None, None, None, 0, None, None, None, 0, None, None, None, None) == 1
 
 
 def test_package_refuses_to_run_without_gpu(libfia_path):

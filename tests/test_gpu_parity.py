@@ -421,3 +421,34 @@ def test_mf_item_run_schedule_variant():
                        text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout and "deselected" in r.stdout
+
+
+@pytest.mark.parametrize("name", ["small_mf_k16.npz", "small_ncf_k16.npz"])
+def test_cached_inverse_hvp_force_refresh_false(name, tmp_path):
+    """get_influence_on_test_loss(force_refresh=False) with the reference's cached
+    <model>-cg-normal_loss-test-[t].npz present scores with the cached vector
+    (matrix_factorization.py:210-214) on the GPU (fia_query_batch_x): the cache the first
+    call wrote gives bitwise-identical influence, and a doubled vector exactly doubled
+    influence (influence is linear in x; a power-of-two scale is exact in fp64)."""
+    f = load(name)
+    model = "MF" if "mf" in name else "NCF"
+    k, U, I = int(f["k"]), int(f["U"]), int(f["I"])
+    m = make_model(model, U, I, k, (f["train_user"], f["train_item"], f["train_rating"]),
+                   (f["q_user"], f["q_item"]), params_of(f), tmpdir=tmp_path)
+    t = 0
+    n_tr = f["train_user"].size
+    first = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=True)
+    x0 = np.concatenate([np.ravel(a) for a in m.inverse_hvp])
+    again = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=False)
+    assert np.array_equal(again.view(np.int64), first.view(np.int64))
+    fname = os.path.join(str(tmp_path), "test_%s-cg-normal_loss-test-[%d].npz" % (model, t))
+    with np.load(fname, allow_pickle=False) as z:
+        cached = z["inverse_hvp"]
+    np.savez(fname, inverse_hvp=2.0 * cached)
+    twice = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=False)
+    assert np.array_equal(twice, 2.0 * first)
+    x1 = np.concatenate([np.ravel(a) for a in m.inverse_hvp])
+    assert np.array_equal(x1, 2.0 * x0)
+    # force_refresh=True ignores (and rewrites) the cache
+    fresh = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=True)
+    assert np.array_equal(fresh.view(np.int64), first.view(np.int64))
