@@ -63,6 +63,18 @@ struct NCFm {
 
 __device__ __forceinline__ int tri(int r, int c) { return (r * (r + 1)) / 2 + c; }
 
+// Gram cache element (R >= C) of one side block.  Packed lower triangle, except NCF k = 16
+// (Ds = 32), kept in the row-pair layout of k_solve_rows: lane t of a side system owns rows t
+// and 31 - t, slot C of row t and slot 32 - C of row 31 - t (33 slots per lane), element
+// slot * 16 + t -- one slot of the system's 16 lanes is one 128-B line.
+template <class M>
+__device__ __forceinline__ int gidx(int R, int C) {
+  if constexpr (M::ncf && M::Ds == 32) return R < 16 ? C * 16 + R : (32 - C) * 16 + (31 - R);
+  else return tri(R, C);
+}
+template <class M>
+constexpr bool pair_layout() { return M::ncf && M::Ds == 32; }
+
 // 4 doubles per lane: an f64 MFMA 16x16 tile (C/D layout: element (4 r + (l >> 4), l & 15) in [r])
 typedef double d4_t __attribute__((ext_vector_type(4)));
 
@@ -355,7 +367,7 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
 #pragma unroll
     for (int r = 0; r < N; ++r) {
       const int hi = r > c ? r : c, lo = r > c ? c : r;
-      col[r] = live ? s2n * Gb[tri(hi, lo)] : 0.0;
+      col[r] = live ? s2n * Gb[gidx<M>(hi, lo)] : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < N; ++r)
@@ -363,7 +375,7 @@ __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* _
     double y = live ? g[b * N + c] : 0.0;
     double dinv_own = 0.0;
     // EXTRA: the bias coordinate's pivot and right-hand side (identical in every lane)
-    double d_x = EXTRA ? s2n * Gb[tri(N - 1, N - 1)] + (M::decayed(N - 1) ? wd : 0.0) + damping : 0.0;
+    double d_x = EXTRA ? s2n * Gb[gidx<M>(N - 1, N - 1)] + (M::decayed(N - 1) ? wd : 0.0) + damping : 0.0;
     double y_x = EXTRA ? g[b * N + N - 1] : 0.0;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
@@ -661,10 +673,10 @@ __global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(
       const int c = t - tri(r, 0);
       double h = 0.0;
       if (r < Ds) {
-        h = s2n * (Gu[tri(r, c)] + cdup * g[r] * g[c]);
+        h = s2n * (Gu[gidx<M>(r, c)] + cdup * g[r] * g[c]);
       } else if (c >= Ds) {
         const int rr = r - Ds, cc = c - Ds;
-        h = s2n * (Gi[tri(rr, cc)] + cdup * g[r] * g[c]);
+        h = s2n * (Gi[gidx<M>(rr, cc)] + cdup * g[r] * g[c]);
       } else if (coupled) {
         // cross block: item row rr, user col c: 2 (c g_i g_u^T + esum * d2r/dtheta_i dtheta_u)
         const int rr = r - Ds;
@@ -811,9 +823,11 @@ __device__ constexpr int ut(int p, int j) { return p * NT - (p * (p - 1)) / 2 + 
 // Raw loads of one side system (issued together, ahead of the query's dependent prologue):
 // the upper tiles of the entity's packed lower Gram G (Ds = NM, + 1 with the MF bias), and
 // for the MF bias the bias row at the lane's rows (hr) and column (hc) and its diagonal (hb)
-template <int NT, bool EXTRA>
+template <int NT, bool EXTRA, bool PAIR = false>
 __device__ __forceinline__ void tile_load(const double* __restrict__ G, int g, int c, d4_t (&U)[NT * (NT + 1) / 2],
                                           d4_t (&hr)[NT], double (&hc)[NT], double& hb) {
+  // PAIR: NCF k = 16's row-pair Gram layout (gidx)
+  auto at = [](int R, int C) { return PAIR ? (R < 16 ? C * 16 + R : (32 - C) * 16 + (31 - R)) : (R * (R + 1)) / 2 + C; };
   constexpr int NM = 16 * NT;
   const double* __restrict__ hrow = G + NM * (NM + 1) / 2;   // MF: packed row NM = the bias row
 #pragma unroll
@@ -825,10 +839,10 @@ __device__ __forceinline__ void tile_load(const double* __restrict__ G, int g, i
       for (int j = p; j < NT; ++j) {
         const int C = 16 * j + c;
         if (j > p) {
-          U[ut<NT>(p, j)][r] = G[(C * (C + 1)) / 2 + R];
+          U[ut<NT>(p, j)][r] = G[at(C, R)];
         } else {
           const int hi = R > C ? R : C, lo = R > C ? C : R;
-          U[ut<NT>(p, j)][r] = G[(hi * (hi + 1)) / 2 + lo];
+          U[ut<NT>(p, j)][r] = G[at(hi, lo)];
         }
       }
       if constexpr (EXTRA) hr[p][r] = hrow[R];
@@ -1030,7 +1044,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(tile_waves<
     // NT >= 3 holding the raw tiles across the prologue spills (MF k=64: 0.42 vs 0.35 ms), so
     // they are issued after it
     constexpr bool EARLY = NT <= 2;
-    if constexpr (EARLY) tile_load<NT, EXTRA>(A.gram[wv] + (int64_t)ent * GSP, lg, lc, U, hr, hc, hb);
+    if constexpr (EARLY) tile_load<NT, EXTRA, pair_layout<M>()>(A.gram[wv] + (int64_t)ent * GSP, lg, lc, U, hr, hc, hb);
     if constexpr (EXTRA) {                             // MF rhs: [other side's embedding ; 1]
       const float* __restrict__ Eo = A.t[wv ? 0 : 1] + (int64_t)(wv ? uu : ii) * K;
 #pragma unroll
@@ -1065,7 +1079,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(tile_waves<
       }
       continue;
     }
-    if constexpr (!EARLY) tile_load<NT, EXTRA>(A.gram[wv] + (int64_t)ent * GSP, lg, lc, U, hr, hc, hb);
+    if constexpr (!EARLY) tile_load<NT, EXTRA, pair_layout<M>()>(A.gram[wv] + (int64_t)ent * GSP, lg, lc, U, hr, hc, hb);
     tile_factor<NT, EXTRA>(lg, lc, U, Rt, hr, hc, hb, gam, s2n, A.wd, A.damping, xs + wv * Ds, &Pv[wv][0]);
     __syncthreads();
     if (wv == 0) solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, xs, w, rec + q * M::R, x_out);
@@ -1317,8 +1331,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
     for (int r = 0; r < N; ++r) {
       const int h0 = r > ca ? r : ca, l0 = r > ca ? ca : r;
       const int h1 = r > cb ? r : cb, l1 = r > cb ? cb : r;
-      c0[r] = Gb[tri(h0, l0)];
-      c1[r] = Gb[tri(h1, l1)];
+      c0[r] = Gb[gidx<M>(h0, l0)];
+      c1[r] = Gb[gidx<M>(h1, l1)];
     }
     const int64_t n = s_n[qs];
     // H_b = (2/n) Gram_b + (wd + damping) I  (every NCF coordinate is decayed); n = 0: the
@@ -1404,6 +1418,274 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
            (int)blockIdx.x, iters, st[1], st[2], st[3], st[4], st[5], st[6], st[0]);
 #endif
 #undef STAMP
+}
+
+// ------------------------------------------------------------------------------------
+// NCF k = 16 side-system solve by rows (the default for NCF k = 16), two launches:
+//  k_ncf_query_pro: one THREAD per query -- n, the pair-set lookup, r-hat(u,i) and
+//    v = d r-hat / d theta_t in block order (ncf:102-145, 181-191; gnn:155) into
+//    qpro[q] = {v[D] | r-hat, n, c_dup, 0}.  The MLP is ~0.8 k FMAs per query; computed
+//    wave-cooperatively inside the solve (k_solve_col) it took a fifth of that kernel
+//    (LDS round trips between tiny loops, FIA_STAMPS).
+//  k_solve_rows: 16 lanes per side system (4 systems = 2 queries per wave); lane t owns rows
+//    t and 31 - t of the lower triangle, 33 entries, loaded from the Gram's row-pair layout
+//    (gidx: one 128-B line per slot and system).  Right-looking LDL^T: step J publishes the
+//    pivot column through LDS and every lane updates its two rows; a row's entries live in
+//    a[16] (row t) / b[32] (row 31 - t), slots past a row's end are scratch, so no FMA needs
+//    a mask -- 616 FMAs per lane for the 4 systems (the column layout's full-column updates:
+//    992) at 96 VGPRs of matrix instead of 128 + spills.  Column J + 1 is updated and
+//    published before the rest of step J, so the LDS round trip overlaps those FMAs; the
+//    forward solve rides along, the backward solve is one 16-lane DPP sum per row.
+// ------------------------------------------------------------------------------------
+template <class M>
+constexpr int qpro_stride() { return M::D + 4; }
+#ifndef FIA_ROWS_RG
+#define FIA_ROWS_RG 8
+#endif
+#ifndef FIA_ROWS_WAVES
+#define FIA_ROWS_WAVES 3
+#endif
+constexpr int kRowsRG = FIA_ROWS_RG;      // pivot reads per group (A/B build knob)
+
+template <class M>
+__global__ __launch_bounds__(64) void k_ncf_query_pro(QueryArgs A, int64_t Q, double* __restrict__ qpro) {
+  constexpr int K = M::K, H2 = K / 2, Ds = M::Ds, D = M::D, PS = qpro_stride<M>();
+  const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (q >= Q) return;
+  const int32_t u = A.qu[q], i = A.qi[q];
+  const bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
+  const int32_t uu = ok ? u : 0, ii = ok ? i : 0;         // clamped ids (n = 0 for invalid ones)
+  const int64_t n = ok ? (A.ptr[0][uu + 1] - A.ptr[0][uu]) + (A.ptr[1][ii + 1] - A.ptr[1][ii]) : 0;
+  double cdup, rsum;
+  A.pairs.lookup((unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii, cdup, rsum);
+  const float* __restrict__ W1 = A.t[4];
+  const float* __restrict__ b1 = A.t[5];
+  const float* __restrict__ W2 = A.t[6];
+  const float* __restrict__ b2 = A.t[7];
+  const float* __restrict__ W3 = A.t[8];
+  const double* __restrict__ l1u = A.l1[0] + (int64_t)uu * K;
+  const double* __restrict__ l1i = A.l1[1] + (int64_t)ii * K;
+  double z1[K];
+#pragma unroll
+  for (int a = 0; a < K; ++a) z1[a] = l1u[a] + l1i[a] + (double)b1[a];
+  double d2[H2], rh = 0.0;
+#pragma unroll
+  for (int e = 0; e < H2; ++e) {
+    double z2 = (double)b2[e];
+#pragma unroll
+    for (int c = 0; c < K; ++c) z2 = fma((double)W2[c * H2 + e], z1[c] > 0.0 ? z1[c] : 0.0, z2);
+    const bool on = z2 > 0.0;
+    d2[e] = on ? (double)W3[e] : 0.0;
+    rh += on ? (double)W3[e] * z2 : 0.0;
+  }
+  double* __restrict__ P = qpro + q * PS;
+  const float* __restrict__ pg = A.t[2] + (int64_t)uu * K;
+  const float* __restrict__ qg = A.t[3] + (int64_t)ii * K;
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const double w3g = (double)W3[H2 + a], pga = (double)pg[a], qga = (double)qg[a];
+    rh += w3g * pga * qga;
+    P[K + a] = w3g * qga;              // d r / d Pg_u = W3g * Qg_i
+    P[Ds + K + a] = w3g * pga;         // d r / d Qg_i = W3g * Pg_u
+  }
+  double d1[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < H2; ++e) s = fma((double)W2[c * H2 + e], d2[e], s);
+    d1[c] = z1[c] > 0.0 ? s : 0.0;
+  }
+#pragma unroll
+  for (int a = 0; a < 2 * K; ++a) {    // rows a < K: W1[:k] (user block), a >= K: W1[k:] (item block)
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < K; ++c) s = fma((double)W1[a * K + c], d1[c], s);
+    P[a < K ? a : Ds + (a - K)] = s;
+  }
+  P[D] = rh + (double)A.t[9][0];
+  P[D + 1] = (double)n;
+  P[D + 2] = cdup;
+  P[D + 3] = 0.0;
+}
+
+// Step J of k_solve_rows.  P0 / P1: the pivot slots of even / odd steps ([0, 32) the
+// column's rows, 32 y_J); lt / lb: the multipliers of rows t / 31 - t (0 unless the row is
+// strictly below the pivot, so finished rows and the pivot row take no update).
+template <int J>
+__device__ __forceinline__ void rows_step(double (&a)[16], double (&b)[32], double& yt, double& yb, double& dit,
+                                          double& dib, int t, double* __restrict__ P0, double* __restrict__ P1) {
+  const double* __restrict__ Pb = (J & 1) ? P1 : P0;
+  double* __restrict__ Pn = (J & 1) ? P0 : P1;
+  const int tb = 31 - t;
+  wave_lds_sync();
+  const double dj = Pb[J], yj = Pb[32];
+  double ij = __builtin_amdgcn_rcp(dj);            // 1/d_J: v_rcp_f64 + two Newton steps
+  ij = fma(ij, fma(-dj, ij, 1.0), ij);
+  ij = fma(ij, fma(-dj, ij, 1.0), ij);
+  double lt = 0.0;
+  if constexpr (J < 16) lt = t > J ? a[J] * ij : 0.0;
+  const double lb = tb > J ? b[J] * ij : 0.0;
+  if (t == J) dit = ij;
+  if (tb == J) dib = ij;
+  yt = fma(-lt, yj, yt);
+  yb = fma(-lb, yj, yb);
+  if constexpr (J + 1 < 32) {
+    // column J + 1 first, then published for step J + 1 (with y_{J+1} by its owner)
+    const double p = Pb[J + 1];
+    if constexpr (J + 1 < 16) {
+      a[J + 1] = fma(-lt, p, a[J + 1]);
+      Pn[t] = a[J + 1];
+    }
+    b[J + 1] = fma(-lb, p, b[J + 1]);
+    Pn[tb] = b[J + 1];
+    if constexpr (J + 1 < 16) {
+      if (t == J + 1) Pn[32] = yt;
+    } else {
+      if (tb == J + 1) Pn[32] = yb;
+    }
+  }
+  // the pivot reads in groups of RG columns (a compiler barrier between groups): all of a
+  // step's reads hoisted together hold 62 more VGPRs
+#pragma unroll
+  for (int c = J + 2; c < 16; ++c) {
+    if ((c - J - 2) % kRowsRG == kRowsRG - 1) asm volatile("" ::: "memory");
+    const double p = Pb[c];
+    a[c] = fma(-lt, p, a[c]);
+    b[c] = fma(-lb, p, b[c]);
+  }
+#pragma unroll
+  for (int c = (J + 2 > 16 ? J + 2 : 16); c < 32; ++c) {
+    if ((c - J - 2) % kRowsRG == kRowsRG - 1) asm volatile("" ::: "memory");
+    b[c] = fma(-lb, Pb[c], b[c]);
+  }
+  if constexpr (J < 16) a[J] = lt;                 // L[t][J], L[31 - t][J]
+  b[J] = lb;
+  // materialise this step's updates here (hipcc otherwise sinks each row's FMA to the step
+  // that first needs it and keeps every step's multipliers live: spills)
+#pragma unroll
+  for (int c = (J < 16 ? J : 16); c < 16; ++c) asm volatile("" : "+v"(a[c]));
+#pragma unroll
+  for (int c = J; c < 32; ++c) asm volatile("" : "+v"(b[c]));
+  asm volatile("" : "+v"(yt), "+v"(yb));
+}
+
+template <int J>
+__device__ __forceinline__ void rows_steps(double (&a)[16], double (&b)[32], double& yt, double& yb, double& dit,
+                                           double& dib, int t, double* __restrict__ P0, double* __restrict__ P1) {
+  if constexpr (J < 32) {
+    rows_step<J>(a, b, yt, yb, dit, dib, t, P0, P1);
+    rows_steps<J + 1>(a, b, yt, yb, dit, dib, t, P0, P1);
+  }
+}
+
+// L^T x = z from the last row: x_J = z_J - sum_{r > J} L[r][J] x_r, the sum over the system's
+// 16 lanes (each holds L[t][J] x_t + L[31-t][J] x_{31-t}; 0 for rows not below J)
+template <int J>
+__device__ __forceinline__ void rows_back(const double (&a)[16], const double (&b)[32], double zt, double zb,
+                                          double& xt, double& xb, int t) {
+  if constexpr (J >= 0) {
+    double s = b[J] * xb;
+    if constexpr (J < 16) s = fma(a[J], xt, s);
+    s = row_sum16(s);
+    if constexpr (J < 16) {
+      if (t == J) xt = zt - s;
+    } else {
+      if (31 - t == J) xb = zb - s;
+    }
+    rows_back<J - 1>(a, b, zt, zb, xt, xb, t);
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FIA_ROWS_WAVES))) void k_solve_rows(
+    QueryArgs A, int64_t Q, const double* __restrict__ qpro, double* __restrict__ rec, double* __restrict__ x_out,
+    int32_t* __restrict__ coupled_out) {
+  static_assert(pair_layout<M>(), "NCF k = 16 (side blocks of 32)");
+  constexpr int K = M::K, H2 = K / 2, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  constexpr int PS = qpro_stride<M>(), PST = 36;   // 36 doubles: the 4 systems' slots in distinct banks
+  __shared__ double Pv[2][4 * PST];
+  const int lane = threadIdx.x, sys = lane >> 4, t = lane & 15, h = sys >> 1, sd = sys & 1, tb = 31 - t;
+  const int64_t q = (int64_t)blockIdx.x * 2 + h;
+  const bool qok = q < Q;
+  const int64_t qc = qok ? q : Q - 1;
+  const int32_t u = A.qu[qc], i = A.qi[qc];
+  const bool okid = u >= 0 && u < A.U && i >= 0 && i < A.I;
+  const int32_t uu = okid ? u : 0, ii = okid ? i : 0;
+  const int32_t ent = sd ? ii : uu;
+  const double* __restrict__ Gb = A.gram[sd] + (int64_t)ent * GSP + t;
+  const double* __restrict__ P = qpro + qc * PS;
+  double a[16], b[32];
+#pragma unroll
+  for (int s = 0; s <= 32; ++s) {                 // slot s: row t col s | row 31 - t col 32 - s
+    const double v = Gb[s * 16];
+    if (s < 16) a[s] = v;
+    if (s >= 1) b[32 - s] = v;
+  }
+  const double nd = P[D + 1];
+  // H_b = (2/n) Gram_b + (wd + damping) I  (every NCF coordinate is decayed); n = 0: the
+  // system is garbage and its query writes NaN below
+  const double s2n = nd > 0.0 ? 2.0 / nd : 0.0;
+  const double lam = A.wd + A.damping;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) a[c] *= s2n;
+#pragma unroll
+  for (int c = 0; c < 32; ++c) b[c] *= s2n;
+#pragma unroll
+  for (int c = 0; c < 16; ++c)
+    if (c == t) a[c] += lam;
+#pragma unroll
+  for (int c = 16; c < 32; ++c)
+    if (c == tb) b[c] += lam;
+  double yt = P[sd * Ds + t], yb = P[sd * Ds + tb], dit = 0.0, dib = 0.0;
+  double* __restrict__ P0 = &Pv[0][sys * PST];
+  double* __restrict__ P1 = &Pv[1][sys * PST];
+  P0[t] = a[0];
+  P0[tb] = b[0];
+  if (t == 0) P0[32] = yt;
+  rows_steps<0>(a, b, yt, yb, dit, dib, t, P0, P1);
+  const double zt = yt * dit, zb = yb * dib;
+  double xt = 0.0, xb = 0.0;
+  rows_back<31>(a, b, zt, zb, xt, xb, t);
+  // ---- record + x_out (record layout: solve_epilogue); sums over the query's 2 systems ----
+  // (loaded here, not held across the factorization)
+  const double rh = P[D], cdup = P[D + 2];
+  const double gt = P[sd * Ds + t], gbv = P[sd * Ds + tb];
+  // theta at the lane's two coordinates: side 0 [Pm_u | Pg_u], side 1 [Qm_i | Qg_i]
+  const double tht = (double)A.t[sd][(int64_t)ent * K + t];
+  const double thb = (double)A.t[2 + sd][(int64_t)ent * K + (tb - K)];
+  const double w3b = (double)A.t[8][H2 + (tb - K)];
+  double cq = fma(xt, tht, xb * thb);
+  double xv = fma(xt, gt, xb * gbv);
+  cq = sys_sum<16>(cq);
+  xv = sys_sum<16>(xv);
+  const int64_t n = (int64_t)nd;
+  if (qok && n > 0 && !(cdup > 0.0)) {
+    double* __restrict__ R = rec + q * M::R;
+    double* __restrict__ S = R + 4 + sd * M::SB;
+    if (sd == 0 && t == 0) {
+      R[0] = 1.0 / nd;
+      R[1] = cq * A.wd;
+      R[2] = xv;
+      R[3] = rh;
+    }
+    S[t] = xt;                                     // x_mlp
+    S[tb] = w3b * xb;                              // W3g * x_gmf
+    if (t == 0) S[2 * K] = (double)(sd ? uu : ii);
+    if (x_out) {
+      x_out[q * D + M::ref_index(sd * Ds + t)] = xt;
+      x_out[q * D + M::ref_index(sd * Ds + tb)] = xb;
+    }
+  } else if (qok && n == 0) {
+    if (x_out) {
+      x_out[q * D + sd * Ds + t] = NAN;
+      x_out[q * D + sd * Ds + tb] = NAN;
+    }
+    if (sd == 0 && t == 0) rec[q * M::R] = NAN;
+  } else if (qok && sd == 0 && t == 0) {          // coupled: the full-D solve finishes it
+    const int slot = atomicAdd(coupled_out, 1);
+    coupled_out[1 + slot] = (int32_t)q;
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1959,7 +2241,7 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
         for (int rr = 0; rr < 4; ++rr) {
           const int ci = 16 * ta + kq + 4 * rr;    // C row -> Gram column index (tile ta)
           const int rj = 16 * tb + m;              // C col -> Gram row index (tile tb)
-          if (rj >= ci) out[tri(rj, ci)] = acc[p][rr];
+          if (rj >= ci) out[gidx<M>(rj, ci)] = acc[p][rr];
         }
   }
 }
@@ -2877,10 +3159,12 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
         cpos[r] = (int32_t)(p0 + sd * (q01.y - q01.x));
 #ifndef FIA_MFMA_NO_ROT
         // aligned stores: the run starts dl elements into a 16-element (128-B influence,
-        // 64-B train-row) segment; lane cn stores segment element cn
+        // 64-B train-row) segment; lane cn stores segment element cn.  (-DFIA_MFMA_NO_ROT:
+        // plain per-tile stores, same outputs; same-box A/B at 20M MF k=64: 3.03 ms per
+        // batch vs 3.13 ms rotated)
         dl[r] = (int)((ob - cn) & 15);
-        outp[r] = influence + (ob - dl[r]);
-        relp[r] = rel_idx + (ob - dl[r]);
+        outp[r] = influence + (ob - cn - dl[r]);   // the aligned segment (lane cn adds cn)
+        relp[r] = rel_idx + (ob - cn - dl[r]);
 #else
         outp[r] = influence + ob;
         relp[r] = rel_idx + ob;
@@ -2904,8 +3188,8 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
         cpos[r] = (int32_t)(p0 + (sd ? qb[1] - qb[0] : 0));  // |R_u| precedes item-side positions
 #ifndef FIA_MFMA_NO_ROT
         dl[r] = (int)((ob - cn) & 15);
-        outp[r] = influence + (ob - dl[r]);
-        relp[r] = rel_idx + (ob - dl[r]);
+        outp[r] = influence + (ob - cn - dl[r]);   // the aligned segment (lane cn adds cn)
+        relp[r] = rel_idx + (ob - cn - dl[r]);
 #else
         outp[r] = influence + ob;
         relp[r] = rel_idx + ob;
@@ -3360,11 +3644,12 @@ constexpr bool use_col_solve() {
   return M::ncf && 2 * M::Ds <= 64;
 }
 
-// side-system solve (A/B knob FIA_SOLVE): default = k_solve_col (NCF k <= 16) / k_solve_tile,
-// tile = k_solve_tile everywhere, cols = the previous one-column-per-lane k_solve
+// side-system solve (A/B knob FIA_SOLVE): default = k_solve_rows (NCF k = 16) / k_solve_col
+// (NCF k = 8) / k_solve_tile, col = k_solve_col for NCF k = 16, tile = k_solve_tile
+// everywhere, cols = the previous one-column-per-lane k_solve
 static int solve_mode() {
   static const char* e = getenv("FIA_SOLVE");
-  static const int m = !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "tile") ? 2 : 0;
+  static const int m = !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "tile") ? 2 : !strcmp(e, "col") ? 3 : 0;
   return m;
 }
 
@@ -3527,7 +3812,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       if constexpr (use_tps<M>())
         hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                            c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
-    } else if (use_col_solve<M>() && solve_mode() == 0) {
+    } else if (pair_layout<M>() && solve_mode() == 0) {
+      if constexpr (pair_layout<M>()) {
+        FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
+        hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(64), 0, s, A, Q,
+                           c->qwork.as<double>());
+        hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
+                           (const double*)c->qwork.as<double>(), c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+      }
+    } else if (use_col_solve<M>() && (solve_mode() == 0 || solve_mode() == 3)) {
       if constexpr (use_col_solve<M>()) {
         static const int64_t genv = getenv("FIA_SOLVE_GRID") ? atoll(getenv("FIA_SOLVE_GRID")) : 0;  // A/B knob
         const int64_t cap = genv > 0 ? genv : (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;

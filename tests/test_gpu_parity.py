@@ -428,8 +428,10 @@ def test_cached_inverse_hvp_force_refresh_false(name, tmp_path):
     """get_influence_on_test_loss(force_refresh=False) with the reference's cached
     <model>-cg-normal_loss-test-[t].npz present scores with the cached vector
     (matrix_factorization.py:210-214) on the GPU (fia_query_batch_x): the cache the first
-    call wrote gives bitwise-identical influence, and a doubled vector exactly doubled
-    influence (influence is linear in x; a power-of-two scale is exact in fp64)."""
+    call wrote gives the same influence up to the rounding of the record's x . theta and
+    x . v sums (k_record_x sums them in another order than the solve kernels: 1e-12
+    relative), and a doubled vector exactly doubled influence (same kernel; influence is
+    linear in x, a power-of-two scale is exact in fp64)."""
     f = load(name)
     model = "MF" if "mf" in name else "NCF"
     k, U, I = int(f["k"]), int(f["U"]), int(f["I"])
@@ -440,13 +442,13 @@ def test_cached_inverse_hvp_force_refresh_false(name, tmp_path):
     first = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=True)
     x0 = np.concatenate([np.ravel(a) for a in m.inverse_hvp])
     again = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=False)
-    assert np.array_equal(again.view(np.int64), first.view(np.int64))
+    assert np.abs(again - first).max() <= 1e-12 * np.abs(first).max()
     fname = os.path.join(str(tmp_path), "test_%s-cg-normal_loss-test-[%d].npz" % (model, t))
     with np.load(fname, allow_pickle=False) as z:
         cached = z["inverse_hvp"]
     np.savez(fname, inverse_hvp=2.0 * cached)
     twice = m.get_influence_on_test_loss([t], np.arange(n_tr), force_refresh=False)
-    assert np.array_equal(twice, 2.0 * first)
+    assert np.array_equal(twice, 2.0 * again)
     x1 = np.concatenate([np.ravel(a) for a in m.inverse_hvp])
     assert np.array_equal(x1, 2.0 * x0)
     # force_refresh=True ignores (and rewrites) the cache
