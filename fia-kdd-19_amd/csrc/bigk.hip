@@ -1045,12 +1045,18 @@ __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list
 
 template <class M, int NP, int NBE>
 __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __restrict__ list, int w0, int c0,
-                                                  int tpb, const double* __restrict__ qwork,
+                                                  int tpb, int nsys, const double* __restrict__ qwork,
                                                   double* __restrict__ lscr) {
   constexpr int LDR = NP + 16, NB = kBsNB, LT = NB + 1, MG = kBsMG, PDT = 5, NT = NBE / 16;
   __shared__ double Pw[4][16 * LT];
   __shared__ double Ws[NB * NB];
-  const int sys = (int)blockIdx.x / tpb, grp = (int)blockIdx.x - sys * tpb;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so physical block b
+  // runs on XCD b % 8 (up to which XCD block 0 gets); all groups of system sys share the
+  // XCD of block sys % 8, so the panel rows every group of a system reads (the B operand)
+  // are one XCD's L2 lines instead of up to eight copies fetched by eight L2s
+  const int xcd = (int)blockIdx.x & 7, jx = (int)blockIdx.x >> 3;
+  const int sys = xcd + 8 * (jx / tpb), grp = jx % tpb;
+  if (sys >= nsys) return;
   const int w = w0 + sys;
   if (w >= list[0]) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
@@ -1798,8 +1804,8 @@ hipError_t launch_bs_panel(fia_ctx* c, const BigArgs& A, int64_t w0, int64_t n, 
   FIA_HIP_TRY(hipGetLastError());
   const int tiles = (NP + 16 - c0 - NBE) / 16;
   const int tpb = (tiles + 4 * kBsMG - 1) / (4 * kBsMG);
-  hipLaunchKernelGGL((k_bs_trail<M, NP, NBE>), dim3((unsigned)(n * tpb)), dim3(256), 0, s, A, list, (int)w0, c0, tpb,
-                     c->qwork.as<double>(), c->lscr.as<double>());
+  hipLaunchKernelGGL((k_bs_trail<M, NP, NBE>), dim3((unsigned)(8 * ((n + 7) / 8) * tpb)), dim3(256), 0, s, A, list,
+                     (int)w0, c0, tpb, (int)n, c->qwork.as<double>(), c->lscr.as<double>());
   return hipGetLastError();
 }
 

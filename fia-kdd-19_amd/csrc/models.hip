@@ -74,6 +74,13 @@ __device__ __forceinline__ int gidx(int R, int C) {
 }
 template <class M>
 constexpr bool pair_layout() { return M::ncf && M::Ds == 32; }
+// NCF k <= 16: per list position the Gram pass stores the two ReLU masks of the MLP (bits
+// [0, k) z1 > 0, [k, 3k/2) z2 > 0: 4 B) instead of g_mlp (8k B); scoring rebuilds
+// d1 = 1[z1 > 0] (W2 (1[z2 > 0] W3m)) from a 2^(k/2)-row LDS table and dots it with
+// y = W1_side^T x_mlp (the record's MLP block after k_ncf_rec_y), since
+// x_mlp . g_mlp = x_mlp . (W1_side d1) = (W1_side^T x_mlp) . d1
+template <class M>
+constexpr bool mask_path() { return M::ncf && M::K <= 16; }
 
 // 4 doubles per lane: an f64 MFMA 16x16 tile (C/D layout: element (4 r + (l >> 4), l & 15) in [r])
 typedef double d4_t __attribute__((ext_vector_type(4)));
@@ -2108,6 +2115,7 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
     const double* __restrict__ Ls = (sd ? l1i : l1u) + (int64_t)e * K;
     const double* __restrict__ L1o = sd ? l1u : l1i;
     double* __restrict__ lgp = const_cast<double*>(GSd.lgm[sd]) + lb;
+    int32_t* __restrict__ lmk = reinterpret_cast<int32_t*>(const_cast<double*>(GSd.lgm[sd])) + lb;   // mask path
     double* __restrict__ lrp = lres + (int64_t)sd * N + lb;
     double zs[KK], gsk[KK];     // own-entity terms for this lane's coordinates
 #pragma unroll
@@ -2186,6 +2194,18 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
 #pragma unroll
         for (int kk = 0; kk < KK; ++kk) gm[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(d1[kk], aW1[t][kk], gm[t], 0, 0, 0);
       }
+      if constexpr (mask_path<M>()) {
+        // ReLU masks of position m: lane (m, kq) holds z1 at c = kq + 4kk and z2 at h = kq + 4r
+        int mk = 0;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) mk |= z1[kk] > 0.0 ? 1 << (kq + 4 * kk) : 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kq + 4 * r < H) mk |= z2[r] + cb2[r] > 0.0 ? 1 << (K + kq + 4 * r) : 0;   // d2's `on`
+        mk |= __shfl_xor(mk, 16);
+        mk |= __shfl_xor(mk, 32);
+        if (kq == 0 && ok) lmk[s0 + m] = mk;
+      }
       // residual of position m (mlp and the gmf dot are split over the 4 lane groups)
       double gmf = 0.0;
 #pragma unroll
@@ -2207,7 +2227,8 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
           double x;
           if (co < K) {
             x = gv;
-            if (okr) lgp[(int64_t)co * N + pr] = gv;
+            if constexpr (!mask_path<M>())
+              if (okr) lgp[(int64_t)co * N + pr] = gv;
           } else {
             x = w3gt[t] * (double)gg[r][t];
           }
@@ -3037,6 +3058,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
 // ------------------------------------------------------------------------------------
 constexpr int kMfmaQB = 15;   // queries per work item (row 15 of A is the entity)
 constexpr int kMfmaCPI = 4;   // list chunks (256 ratings) per work item: the item's setup loads amortised
+#ifndef FIA_MFMA_RING
+#define FIA_MFMA_RING 3
+#endif
+constexpr int kMfmaRing = FIA_MFMA_RING;   // tiles in flight (A/B build knob: 3 or 4)
 
 // output stores of k_score_mf_mfma: 128-B runs of one query per 16 lanes, at the query's
 // arbitrary 8-B alignment; plain stores keep the straddled L2 lines until the next tile
@@ -3057,7 +3082,7 @@ __device__ __forceinline__ long long topk_ikey(double v) {
 }
 
 template <class M, bool FULL, int CPI, int SETUP>
-__global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
+__global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_score_mf_mfma(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
@@ -3207,9 +3232,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
     // software pipeline over the tiles, ring of three slots: the list entries of tile t + 2
     // and the gathered rows of tile t + 1 are in flight while tile t is scored.  Positions
     // past the chunk are clamped to its last entry (harmless loads, no branches).
-    int32_t so[3], sw[3];
-    float sy[3], sbo[3];
-    float4 sb[3][NF4];
+    int32_t so[kMfmaRing], sw[kMfmaRing];
+    float sy[kMfmaRing], sbo[kMfmaRing];
+    float4 sb[kMfmaRing][NF4];
     auto load_list = [&](int t, int k3) {
       const int p = 16 * t + cn < len ? 16 * t + cn : len - 1;
       so[k3] = oth[p];
@@ -3319,21 +3344,47 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
       }
       if (t % TPC == TPC - 1 || t == ntl - 1) emit(t / TPC);
     };
-    load_list(0, 0);
-    load_list(1, 1);
-    gather(0);
-    for (int t = 0; t < ntl; t += 3) {
-      load_list(t + 2, 2);
-      gather(1);
-      tile(t, 0);
-      if (t + 1 >= ntl) break;
-      load_list(t + 3, 0);
-      gather(2);
-      tile(t + 1, 1);
-      if (t + 2 >= ntl) break;
-      load_list(t + 4, 1);
+    if constexpr (kMfmaRing == 4) {
+      // ring of four: list entries 3 tiles and rows 2 tiles ahead
+      load_list(0, 0);
+      load_list(1, 1);
+      load_list(2, 2);
       gather(0);
-      tile(t + 2, 2);
+      gather(1);
+      for (int t = 0; t < ntl; t += 4) {
+        load_list(t + 3, 3);
+        gather(2);
+        tile(t, 0);
+        if (t + 1 >= ntl) break;
+        load_list(t + 4, 0);
+        gather(3);
+        tile(t + 1, 1);
+        if (t + 2 >= ntl) break;
+        load_list(t + 5, 1);
+        gather(0);
+        tile(t + 2, 2);
+        if (t + 3 >= ntl) break;
+        load_list(t + 6, 2);
+        gather(1);
+        tile(t + 3, 3);
+      }
+    } else {
+      load_list(0, 0);
+      load_list(1, 1);
+      gather(0);
+      for (int t = 0; t < ntl; t += 3) {
+        load_list(t + 2, 2);
+        gather(1);
+        tile(t, 0);
+        if (t + 1 >= ntl) break;
+        load_list(t + 3, 0);
+        gather(2);
+        tile(t + 1, 1);
+        if (t + 2 >= ntl) break;
+        load_list(t + 4, 1);
+        gather(0);
+        tile(t + 2, 2);
+      }
     }
 #ifndef FIA_MFMA_NO_ROT
     // the run's tail: the last tile's elements past the last aligned segment
@@ -3346,6 +3397,28 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_mf_mfma(
       }
     }
 #endif
+  }
+}
+
+// NCF k <= 16 (mask path): the record's MLP block x_mlp -> y = W1_side^T x_mlp, one thread
+// per (query, side), after every solve of the batch (k_score_ncf dots y with d1)
+template <class M>
+__global__ __launch_bounds__(256) void k_ncf_rec_y(int64_t Q, const float* __restrict__ W1, double* __restrict__ rec) {
+  constexpr int K = M::K;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * Q) return;
+  const int64_t q = t >> 1;
+  const int sd = (int)(t & 1);
+  double* __restrict__ S = rec + q * M::R + 4 + sd * M::SB;
+  double x[K];
+#pragma unroll
+  for (int a = 0; a < K; ++a) x[a] = S[a];
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    double y = 0.0;
+#pragma unroll
+    for (int a = 0; a < K; ++a) y = fma((double)W1[(sd * K + a) * K + c], x[a], y);
+    S[c] = y;
   }
 }
 
@@ -3365,7 +3438,21 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(M::ncf && M::K % 4 == 0, "NCF, k a multiple of 4");
-  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4;
+  constexpr int K = M::K, RT = kScoreRows, QB = kQueryBlock, CK = 4, H = K / 2;
+  constexpr bool MASK = mask_path<M>();
+  constexpr int TS = K + 1;                        // table row stride (odd: spreads the banks)
+  // mask path: Tm[m2][c] = sum_e W2[c][e] W3m[e] [bit e of m2] = d1[c] / 1[z1_c > 0]
+  __shared__ double Tm[MASK ? (1 << H) * TS : 1];
+  if constexpr (MASK) {
+    for (int t = threadIdx.x; t < (1 << H) * K; t += blockDim.x) {
+      const int m2 = t / K, c = t - m2 * K;
+      double v = 0.0;
+#pragma unroll
+      for (int e = 0; e < H; ++e) v = fma((double)A.t[6][c * H + e], (m2 >> e) & 1 ? (double)A.t[8][e] : 0.0, v);
+      Tm[m2 * TS + c] = v;
+    }
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t n_items = wstart[nE];
@@ -3385,8 +3472,9 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     const float* __restrict__ rat = A.rating[sd] + lb;
     const int32_t* __restrict__ rw = A.row[sd] + lb;
     const double* __restrict__ gml = A.lgm[sd] + lb;
+    const int32_t* __restrict__ lmk = reinterpret_cast<const int32_t*>(A.lgm[sd]) + lb;   // mask path
     const double* __restrict__ res = A.lres + (int64_t)sd * N + lb;
-    int32_t o_[RT], row_[RT], li_[RT];
+    int32_t o_[RT], row_[RT], li_[RT], mk_[RT];
     float y_[RT];
     double ej[RT];
     bool ok_[RT];
@@ -3399,6 +3487,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
       y_[r] = rat[li_[r]];
       row_[r] = rw[li_[r]];
       ej[r] = res[li_[r]];
+      mk_[r] = MASK ? lmk[li_[r]] : 0;
     }
     const float* __restrict__ T = sd == 0 ? A.t[3] : A.t[2];    // other side's gmf table
     // NQ = nq rounded up to a power of two: a static query count per path, so the
@@ -3424,11 +3513,18 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
         // scalar base per coordinate + 32-bit lane offsets (kept opaque so the compiler
         // does not strength-reduce them into 2 VGPRs per (row, coordinate) pointer)
         const double* gbase = gml + (int64_t)c0 * N;
-        asm volatile("" : "+s"(gbase));
+        if constexpr (!MASK) asm volatile("" : "+s"(gbase));
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
+          if constexpr (MASK) {
+            // d1 of rating r at coordinates c0 .. c0 + 3 (mask path; x_mlp is y = W1^T x here)
+            const double* __restrict__ Tr = Tm + (mk_[r] >> K) * TS + c0;
 #pragma unroll
-          for (int cc = 0; cc < CK; ++cc) gm_[r][cc] = gbase[(int64_t)cc * N + li_[r]];
+            for (int cc = 0; cc < CK; ++cc) gm_[r][cc] = (mk_[r] >> (c0 + cc)) & 1 ? Tr[cc] : 0.0;
+          } else {
+#pragma unroll
+            for (int cc = 0; cc < CK; ++cc) gm_[r][cc] = gbase[(int64_t)cc * N + li_[r]];
+          }
           const float4 t = *reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K + c0);
           go_[r][0] = t.x; go_[r][1] = t.y; go_[r][2] = t.z; go_[r][3] = t.w;
         }
@@ -3707,7 +3803,9 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
   if constexpr (M::ncf) {
     // per list position of each side: g_mlp (coordinate-major) and e, with the Grams
     const int64_t N = X.N;
-    for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1), s));
+    // g_mlp coordinate-major [k][N], or (mask path) the ReLU masks int32 [N]
+    const size_t per = mask_path<M>() ? sizeof(int32_t) * (size_t)(N + 2) : sizeof(double) * (size_t)(N * K + 1);
+    for (int sd = 0; sd < 2; ++sd) FIA_HIP_TRY(c->gm[sd].reserve(per, s));
     FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * N + 1), s));
     for (int sd = 0; sd < 2; ++sd) G.lgm[sd] = c->gm[sd].as<double>();
     const int64_t n_all = G.n_items[0] + G.n_items[1];
@@ -3850,6 +3948,12 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     const int64_t g2 = Q < gc ? Q : gc;
     hipLaunchKernelGGL((k_solve<M, false>), dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
                        x_out, (const int32_t*)c->coupled.as<int32_t>(), (int32_t*)nullptr);
+  }
+  if constexpr (mask_path<M>()) {
+    if (Q > 0) {       // the records' MLP block -> y = W1_side^T x_mlp for k_score_ncf
+      hipLaunchKernelGGL(k_ncf_rec_y<M>, dim3((unsigned)((2 * Q + 255) / 256)), dim3(256), 0, s, Q, c->p.t[4],
+                         c->rec.as<double>());
+    }
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
