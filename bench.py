@@ -139,6 +139,8 @@ def solve_kernel(cfg):
         return "k_solve"
     if model == "MF" and k <= 16:
         return "k_solve_tps"
+    if model == "NCF" and k == 16 and mode not in ("tile", "col"):
+        return "k_solve_rows"            # (+ k_ncf_query_pro, the thread-per-query MLP prologue)
     if model == "NCF" and k <= 16 and mode != "tile":
         return "k_solve_col"
     return "k_solve_tile"

@@ -3075,6 +3075,21 @@ __device__ __forceinline__ void st_out(T v, T* p) {
 #endif
 }
 
+// every lane gets lane 48 + (l & 15)'s value (row 3 of a 16x16 f64 MFMA C register, column
+// l & 15): two permlane swaps and selects, no LDS round trip (a ds_bpermute waits ~100+
+// cycles right after the MFMA chain)
+__device__ __forceinline__ double bcast_row3(double x) {
+  const long long b = __double_as_longlong(x);
+  const unsigned lo = (unsigned)(b & 0xffffffffll), hi = (unsigned)(b >> 32);
+  // permlane32_swap(x, x) -> {[r0 r1 r0 r1], [r2 r3 r2 r3]} (rows of 16 lanes)
+  const auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  // permlane16_swap(y, y), y = [r2 r3 r2 r3] -> {[r2 r2 r2 r2], [r3 r3 r3 r3]}
+  const auto l16 = __builtin_amdgcn_permlane16_swap(l32[1], l32[1], false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(h32[1], h32[1], false, false);
+  return __longlong_as_double(((long long)h16[1] << 32) | l16[1]);
+}
+
 __device__ __forceinline__ long long topk_ikey(double v) {
   // |v|'s bits order like |v| (non-negative doubles); NaN ranks below every number
   const long long b = __double_as_longlong(v) & 0x7fffffffffffffffll;
@@ -3242,7 +3257,12 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
       sw[k3] = rw[p];
     };
     auto gather = [&](int k3) {
+#ifdef FIA_ABL_ONE_ROW
+      // ablation (A/B builds only): every gather reads row 0 -- wrong outputs, timing only
+      const float4* row = reinterpret_cast<const float4*>(T + KS * kk);
+#else
       const float4* row = reinterpret_cast<const float4*>(T + (int64_t)so[k3] * K + KS * kk);
+#endif
 #pragma unroll
       for (int f = 0; f < NF4; ++f) sb[k3][f] = row[f];
       sbo[k3] = bt[so[k3]];
@@ -3296,7 +3316,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
       const int32_t o = so[k3], w = sw[k3];
       const double y = (double)sy[k3];
       // residual of rating cn: D[15][cn] lives in lane 48 + cn, register 3
-      const double dself = __shfl(acc[3], 48 + cn);
+      const double dself = bcast_row3(acc[3]);
       const double en = ((dself + bself) + (double)sbo[k3]) + gbias - y;
       const bool dup = pv && (o == dupo[0] || o == dupo[1] || o == dupo[2] || o == dupo[3]);
       double val[4];
@@ -3329,7 +3349,13 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         const int32_t rw = __shfl(w, srcl);
         const bool cur = cn >= dl[r];
         const int idx = 16 * t + cn - dl[r];          // element of the run this lane stores
-        if (qv[r] && (cur ? idx < len : t > 0)) {
+#ifdef FIA_ABL_NO_STORES
+        // ablation (A/B builds only): no output stores -- timing only
+        if (qv[r] && (cur ? idx < len : t > 0) && __double_as_longlong(rv) == 0x7ff8dead0000beefll)
+#else
+        if (qv[r] && (cur ? idx < len : t > 0))
+#endif
+        {
           if (FULL || influence) st_out(cur ? rv : prv[r], outp[r] + 16 * t + cn);
           if (FULL || rel_idx) st_out(cur ? rw : prw[r], relp[r] + 16 * t + cn);
         }
