@@ -1450,14 +1450,23 @@ constexpr int qpro_stride() { return M::D + 4; }
 #define FIA_ROWS_RG 8
 #endif
 #ifndef FIA_ROWS_WAVES
-#define FIA_ROWS_WAVES 3
+#define FIA_ROWS_WAVES 2      // 198 VGPRs, no spills; at 3 waves (168 VGPRs) 34 spill: 0.252 vs 0.220 ms at yelp-ex
 #endif
 constexpr int kRowsRG = FIA_ROWS_RG;      // pivot reads per group (A/B build knob)
 
 template <class M>
-__global__ __launch_bounds__(64) void k_ncf_query_pro(QueryArgs A, int64_t Q, double* __restrict__ qpro) {
+__global__ __launch_bounds__(256) void k_ncf_query_pro(QueryArgs A, int64_t Q, double* __restrict__ qpro) {
   constexpr int K = M::K, H2 = K / 2, Ds = M::Ds, D = M::D, PS = qpro_stride<M>();
-  const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  // the MLP weights as fp64 in LDS, read per use as broadcasts (per-use scalar loads of the
+  // fp32 tables expose a memory latency per weight)
+  __shared__ double sW1[2 * K * K], sW2[K * H2], sW3[3 * H2], sb1[K], sb2[H2];
+  for (int e = threadIdx.x; e < 2 * K * K; e += 256) sW1[e] = (double)A.t[4][e];
+  for (int e = threadIdx.x; e < K * H2; e += 256) sW2[e] = (double)A.t[6][e];
+  for (int e = threadIdx.x; e < 3 * H2; e += 256) sW3[e] = (double)A.t[8][e];
+  for (int e = threadIdx.x; e < K; e += 256) sb1[e] = (double)A.t[5][e];
+  for (int e = threadIdx.x; e < H2; e += 256) sb2[e] = (double)A.t[7][e];
+  __syncthreads();
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (q >= Q) return;
   const int32_t u = A.qu[q], i = A.qi[q];
   const bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
@@ -1465,32 +1474,27 @@ __global__ __launch_bounds__(64) void k_ncf_query_pro(QueryArgs A, int64_t Q, do
   const int64_t n = ok ? (A.ptr[0][uu + 1] - A.ptr[0][uu]) + (A.ptr[1][ii + 1] - A.ptr[1][ii]) : 0;
   double cdup, rsum;
   A.pairs.lookup((unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii, cdup, rsum);
-  const float* __restrict__ W1 = A.t[4];
-  const float* __restrict__ b1 = A.t[5];
-  const float* __restrict__ W2 = A.t[6];
-  const float* __restrict__ b2 = A.t[7];
-  const float* __restrict__ W3 = A.t[8];
   const double* __restrict__ l1u = A.l1[0] + (int64_t)uu * K;
   const double* __restrict__ l1i = A.l1[1] + (int64_t)ii * K;
   double z1[K];
 #pragma unroll
-  for (int a = 0; a < K; ++a) z1[a] = l1u[a] + l1i[a] + (double)b1[a];
+  for (int a = 0; a < K; ++a) z1[a] = l1u[a] + l1i[a] + sb1[a];
   double d2[H2], rh = 0.0;
 #pragma unroll
   for (int e = 0; e < H2; ++e) {
-    double z2 = (double)b2[e];
+    double z2 = sb2[e];
 #pragma unroll
-    for (int c = 0; c < K; ++c) z2 = fma((double)W2[c * H2 + e], z1[c] > 0.0 ? z1[c] : 0.0, z2);
+    for (int c = 0; c < K; ++c) z2 = fma(sW2[c * H2 + e], z1[c] > 0.0 ? z1[c] : 0.0, z2);
     const bool on = z2 > 0.0;
-    d2[e] = on ? (double)W3[e] : 0.0;
-    rh += on ? (double)W3[e] * z2 : 0.0;
+    d2[e] = on ? sW3[e] : 0.0;
+    rh += on ? sW3[e] * z2 : 0.0;
   }
   double* __restrict__ P = qpro + q * PS;
   const float* __restrict__ pg = A.t[2] + (int64_t)uu * K;
   const float* __restrict__ qg = A.t[3] + (int64_t)ii * K;
 #pragma unroll
   for (int a = 0; a < K; ++a) {
-    const double w3g = (double)W3[H2 + a], pga = (double)pg[a], qga = (double)qg[a];
+    const double w3g = sW3[H2 + a], pga = (double)pg[a], qga = (double)qg[a];
     rh += w3g * pga * qga;
     P[K + a] = w3g * qga;              // d r / d Pg_u = W3g * Qg_i
     P[Ds + K + a] = w3g * pga;         // d r / d Qg_i = W3g * Pg_u
@@ -1500,14 +1504,14 @@ __global__ __launch_bounds__(64) void k_ncf_query_pro(QueryArgs A, int64_t Q, do
   for (int c = 0; c < K; ++c) {
     double s = 0.0;
 #pragma unroll
-    for (int e = 0; e < H2; ++e) s = fma((double)W2[c * H2 + e], d2[e], s);
+    for (int e = 0; e < H2; ++e) s = fma(sW2[c * H2 + e], d2[e], s);
     d1[c] = z1[c] > 0.0 ? s : 0.0;
   }
 #pragma unroll
   for (int a = 0; a < 2 * K; ++a) {    // rows a < K: W1[:k] (user block), a >= K: W1[k:] (item block)
     double s = 0.0;
 #pragma unroll
-    for (int c = 0; c < K; ++c) s = fma((double)W1[a * K + c], d1[c], s);
+    for (int c = 0; c < K; ++c) s = fma(sW1[a * K + c], d1[c], s);
     P[a < K ? a : Ds + (a - K)] = s;
   }
   P[D] = rh + (double)A.t[9][0];
@@ -3431,6 +3435,11 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
 template <class M>
 __global__ __launch_bounds__(256) void k_ncf_rec_y(int64_t Q, const float* __restrict__ W1, double* __restrict__ rec) {
   constexpr int K = M::K;
+  // W1 as fp64 in LDS: read per use as a broadcast (the per-use scalar loads of the fp32
+  // table exposed one memory latency per weight: 20 us at yelp-ex)
+  __shared__ double w1[2 * K * K];
+  for (int e = threadIdx.x; e < 2 * K * K; e += 256) w1[e] = (double)W1[e];
+  __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= 2 * Q) return;
   const int64_t q = t >> 1;
@@ -3439,11 +3448,12 @@ __global__ __launch_bounds__(256) void k_ncf_rec_y(int64_t Q, const float* __res
   double x[K];
 #pragma unroll
   for (int a = 0; a < K; ++a) x[a] = S[a];
+  const double* __restrict__ ws = w1 + sd * K * K;
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     double y = 0.0;
 #pragma unroll
-    for (int a = 0; a < K; ++a) y = fma((double)W1[(sd * K + a) * K + c], x[a], y);
+    for (int a = 0; a < K; ++a) y = fma(ws[a * K + c], x[a], y);
     S[c] = y;
   }
 }
@@ -3939,7 +3949,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     } else if (pair_layout<M>() && solve_mode() == 0) {
       if constexpr (pair_layout<M>()) {
         FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
-        hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(64), 0, s, A, Q,
+        hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, A, Q,
                            c->qwork.as<double>());
         hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
                            (const double*)c->qwork.as<double>(), c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
