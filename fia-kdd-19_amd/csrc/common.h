@@ -197,6 +197,7 @@ struct fia_ctx {
   fia::DevBuf wstart;     // int64 [U + I + 1] exclusive scan of the work items per entity
   fia::DevBuf gscan;      // k_group_scan tile words + counters (left zero by every launch)
   fia::DevBuf witems;     // int32 [3 * max items] {global entity, list chunk, query block}
+  fia::DevBuf d1tab;      // NCF k <= 16: d1 per z2 ReLU mask [2^(k/2)][k] (fp64)
   // large-k path (bigk.hip): per-list-position entity, per-train-row residual / NCF backward
   // vectors, per-query Hessian inputs and solutions, solve lists and LDL^T scratch
   fia::DevBuf self[2];    // int32 [N] entity owning list position p of side s

@@ -454,6 +454,7 @@ struct QueryArgs {
   const double* lgm[2];
   const double* lres;
   int64_t N;
+  const double* d1tab;   // NCF k <= 16: d1 table [2^(k/2)][k] (k_ncf_d1_table)
 };
 
 // theta_t, v = d r(u,i)/d theta_t (gnn:155, mf:194,201 / ncf:222,229) and r-hat(u,i) of one
@@ -3430,6 +3431,21 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
   }
 }
 
+// NCF k <= 16 (mask path): T[m][c] = sum_e W2[c][e] W3m[e] [bit e of m], the d1 of a train
+// row whose z2 ReLU mask is m (before its z1 mask), one thread per entry
+template <class M>
+__global__ __launch_bounds__(256) void k_ncf_d1_table(const float* __restrict__ W2, const float* __restrict__ W3,
+                                                      double* __restrict__ tab) {
+  constexpr int K = M::K, H = K / 2;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= (1 << H) * K) return;
+  const int m2 = t / K, c = t - m2 * K;
+  double v = 0.0;
+#pragma unroll
+  for (int e = 0; e < H; ++e) v = fma((double)W2[c * H + e], (m2 >> e) & 1 ? (double)W3[e] : 0.0, v);
+  tab[t] = v;
+}
+
 // NCF k <= 16 (mask path): the record's MLP block x_mlp -> y = W1_side^T x_mlp, one thread
 // per (query, side), after every solve of the batch (k_score_ncf dots y with d1)
 template <class M>
@@ -3461,9 +3477,11 @@ __global__ __launch_bounds__(256) void k_ncf_rec_y(int64_t Q, const float* __res
 // ------------------------------------------------------------------------------------
 // NCF entity-shared scoring.  Same work items, query blocks and outputs as
 // k_score_grouped_mf, but nothing of the MLP is recomputed here: per list position the
-// Gram pass stored g_mlp,j = W1_side . d1_j (coordinate-major, so every load below is a
-// coalesced 512-B wave row) and e_j, and the solve stored x_mlp and W3g * x_gmf, so
-//   s_jq = x_mlp,q . g_mlp,j + (W3g * x_gmf,q) . gmf_other(j)      (ncf:193-280)
+// Gram pass stored e_j and, per list position, the ReLU masks (k <= 16; k = 32: g_mlp,j =
+// W1_side . d1_j coordinate-major, every load a coalesced 512-B wave row), and the solve
+// stored x_mlp (k <= 16: y = W1_side^T x_mlp after k_ncf_rec_y) and W3g * x_gmf, so
+//   s_jq = y_q . d1_j + (W3g * x_gmf,q) . gmf_other(j)  =  x_mlp,q . g_mlp,j + ...   (ncf:193-280)
+// with d1_j from the z1 mask and the table row of the z2 mask (k_ncf_d1_table, in LDS)
 // is 2k FMAs per (rating, query) over the work item's 256 ratings (4 rows per lane).
 // One candidate slot set per work item (spc = 1).
 // ------------------------------------------------------------------------------------
@@ -3480,12 +3498,12 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
   // mask path: Tm[m2][c] = sum_e W2[c][e] W3m[e] [bit e of m2] = d1[c] / 1[z1_c > 0]
   __shared__ double Tm[MASK ? (1 << H) * TS : 1];
   if constexpr (MASK) {
-    for (int t = threadIdx.x; t < (1 << H) * K; t += blockDim.x) {
-      const int m2 = t / K, c = t - m2 * K;
-      double v = 0.0;
-#pragma unroll
-      for (int e = 0; e < H; ++e) v = fma((double)A.t[6][c * H + e], (m2 >> e) & 1 ? (double)A.t[8][e] : 0.0, v);
-      Tm[m2 * TS + c] = v;
+    // the table (k_ncf_d1_table, once per batch) copied in with 16-B loads
+    for (int t = threadIdx.x; t < (1 << H) * K / 2; t += blockDim.x) {
+      const double2 v = reinterpret_cast<const double2*>(A.d1tab)[t];
+      const int e = 2 * t, m2 = e / K, c = e - m2 * K;
+      Tm[m2 * TS + c] = v.x;
+      Tm[m2 * TS + c + 1] = v.y;
     }
     __syncthreads();
   }
@@ -3504,6 +3522,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     const int64_t gb = gstart[g] + (int64_t)qblk * QB;
     const int64_t gn = gstart[g + 1] - gb;
     const int nq = gn < QB ? (int)gn : QB;
+
     const int32_t* __restrict__ oth = A.other[sd] + lb;
     const float* __restrict__ rat = A.rating[sd] + lb;
     const int32_t* __restrict__ rw = A.row[sd] + lb;
@@ -3732,7 +3751,7 @@ __global__ __launch_bounds__(256) void k_topk_merge_thread(
 // host-side dispatch
 // ------------------------------------------------------------------------------------
 QueryArgs make_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
-  QueryArgs A;
+  QueryArgs A{};
   A.qu = qu;
   A.qi = qi;
   A.U = c->p.U;
@@ -3989,6 +4008,11 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     if (Q > 0) {       // the records' MLP block -> y = W1_side^T x_mlp for k_score_ncf
       hipLaunchKernelGGL(k_ncf_rec_y<M>, dim3((unsigned)((2 * Q + 255) / 256)), dim3(256), 0, s, Q, c->p.t[4],
                          c->rec.as<double>());
+      constexpr int NT = (1 << (M::K / 2)) * M::K;
+      FIA_HIP_TRY(c->d1tab.reserve(sizeof(double) * NT, s));
+      hipLaunchKernelGGL(k_ncf_d1_table<M>, dim3((unsigned)((NT + 255) / 256)), dim3(256), 0, s, c->p.t[6], c->p.t[8],
+                         c->d1tab.as<double>());
+      A.d1tab = c->d1tab.as<double>();
     }
   }
   FIA_HIP_TRY(hipGetLastError());
