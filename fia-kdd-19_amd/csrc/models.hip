@@ -3548,29 +3548,32 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
     // NQ = nq rounded up to a power of two: a static query count per path, so the
     // accumulators stay in registers without per-query exits (the padding columns
     // score copies of the last query and are never written out)
-    auto run = [&](auto nq_c) {
+    // RTE = rows per lane actually scored: a chunk of <= 64 ratings (most lists at yelp-ex, ~24
+    // ratings per user or item) runs one row per lane instead of four
+    auto run = [&](auto nq_c, auto rt_c) {
       constexpr int NQ = decltype(nq_c)::value;
+      constexpr int RTE = decltype(rt_c)::value;
       const double* __restrict__ xq[NQ];        // uniform: this side's record block of each query
 #pragma unroll
       for (int j = 0; j < NQ; ++j) {
         const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
         xq[j] = rec + (int64_t)q * M::R + 4 + sd * M::SB;
       }
-      double acc[NQ][RT];
+      double acc[NQ][RTE];
 #pragma unroll
       for (int j = 0; j < NQ; ++j)
 #pragma unroll
-        for (int r = 0; r < RT; ++r) acc[j][r] = 0.0;
+        for (int r = 0; r < RTE; ++r) acc[j][r] = 0.0;
 #pragma unroll 1
       for (int c0 = 0; c0 < K; c0 += CK) {
-        double gm_[RT][CK];
-        float go_[RT][CK];
+        double gm_[RTE][CK];
+        float go_[RTE][CK];
         // scalar base per coordinate + 32-bit lane offsets (kept opaque so the compiler
         // does not strength-reduce them into 2 VGPRs per (row, coordinate) pointer)
         const double* gbase = gml + (int64_t)c0 * N;
         if constexpr (!MASK) asm volatile("" : "+s"(gbase));
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
+        for (int r = 0; r < RTE; ++r) {
           if constexpr (MASK) {
             // d1 of rating r at coordinates c0 .. c0 + 3 (mask path; x_mlp is y = W1^T x here)
             const double* __restrict__ Tr = Tm + (mk_[r] >> K) * TS + c0;
@@ -3591,7 +3594,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
             const double ax = xq[j][c0 + 2 * c2], ay = xq[j][c0 + 2 * c2 + 1];
             const double bx = xq[j][K + c0 + 2 * c2], by = xq[j][K + c0 + 2 * c2 + 1];
 #pragma unroll
-            for (int r = 0; r < RT; ++r) {
+            for (int r = 0; r < RTE; ++r) {
               acc[j][r] = fma(ax, gm_[r][2 * c2], acc[j][r]);
               acc[j][r] = fma(ay, gm_[r][2 * c2 + 1], acc[j][r]);
               acc[j][r] = fma(bx, (double)go_[r][2 * c2], acc[j][r]);
@@ -3610,10 +3613,10 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
         const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
         const int64_t obj = qb[sd] + (int64_t)cidx * kChunk, cbj = qb[2 + sd] + cidx;
         const int64_t poj = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
-        double la[RT], lv[RT];
-        int lp[RT];
+        double la[RTE], lv[RTE];
+        int lp[RTE];
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
+        for (int r = 0; r < RTE; ++r) {
           double ee = ej[r], ss = acc[j][r];
           if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
           const double infl = (2.0 * ee * ss + cq) * inv_n;
@@ -3633,7 +3636,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
             double ba = -2.0, bv = 0.0;
             int bp = 0x7fffffff;
 #pragma unroll
-            for (int r = 0; r < RT; ++r)
+            for (int r = 0; r < RTE; ++r)
               if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
                 ba = la[r]; bp = lp[r]; bv = lv[r];
               }
@@ -3650,10 +3653,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
         }
       }
     };
-    if (nq <= 1) run(std::integral_constant<int, 1>{});
-    else if (nq <= 2) run(std::integral_constant<int, 2>{});
-    else if (nq <= 4) run(std::integral_constant<int, 4>{});
-    else run(std::integral_constant<int, QB>{});
+    auto run_q = [&](auto rt_c) {
+      if (nq <= 1) run(std::integral_constant<int, 1>{}, rt_c);
+      else if (nq <= 2) run(std::integral_constant<int, 2>{}, rt_c);
+      else if (nq <= 4) run(std::integral_constant<int, 4>{}, rt_c);
+      else run(std::integral_constant<int, QB>{}, rt_c);
+    };
+    if (len <= 64) run_q(std::integral_constant<int, 1>{});
+    else run_q(std::integral_constant<int, RT>{});
     __builtin_amdgcn_wave_barrier();
   }
 }
