@@ -2274,7 +2274,7 @@ __global__ __launch_bounds__(64) void k_ncf_gram_rows(GramSides GSd, const float
 
 // Sum the partial Grams of split lists in slot order (deterministic); both sides in one
 // launch (blocks [0, n_comb0) the user side).
-__global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int32_t* __restrict__ comb0,
+__global__ __launch_bounds__(256) void k_gram_combine(int64_t n_comb0, const int32_t* __restrict__ comb0,
                                                      const double* __restrict__ part0, double* __restrict__ gram0,
                                                      int64_t n_comb1, const int32_t* __restrict__ comb1,
                                                      const double* __restrict__ part1, double* __restrict__ gram1,
@@ -2288,19 +2288,18 @@ __global__ __launch_bounds__(64) void k_gram_combine(int64_t n_comb0, const int3
   const int32_t e = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
   if (mark && !mark[(sd ? moff1 : 0) + e]) return;
   // partials summed in slot order (deterministic), their loads issued 8 slots at a time
-  // rather than one dependent round trip per slot
-  for (int t = threadIdx.x; t < GS; t += 64) {
+  // rather than one dependent round trip per slot; the last group's missing slots load slot
+  // `first` and are weighted 0 (branch-free: a partial group is not a chain of round trips)
+  for (int t = threadIdx.x; t < GS; t += blockDim.x) {
     const double* __restrict__ pt = part + (int64_t)first * GSP + t;
     double s = 0.0;
-    int k = 0;
-    for (; k + 8 <= ns; k += 8) {
+    for (int k = 0; k < ns; k += 8) {
       double v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = pt[(int64_t)(k + j) * GSP];
+      for (int j = 0; j < 8; ++j) v[j] = pt[(int64_t)(k + j < ns ? k + j : 0) * GSP];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
+      for (int j = 0; j < 8; ++j) s += k + j < ns ? v[j] : 0.0;
     }
-    for (; k < ns; ++k) s += pt[(int64_t)k * GSP];
     gram[(int64_t)e * GSP + t] = s;
   }
 }
@@ -3906,7 +3905,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
   }
   const int64_t nc0 = n_ent[0] > 0 ? X.n_gcomb[0] : 0, nc1 = n_ent[1] > 0 ? X.n_gcomb[1] : 0;
   if (nc0 + nc1 > 0) {
-    hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)(nc0 + nc1)), dim3(64), 0, s, nc0, X.gcomb[0].as<int32_t>(),
+    hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)(nc0 + nc1)), dim3(256), 0, s, nc0, X.gcomb[0].as<int32_t>(),
                        c->gpart[0].as<double>(), c->gram[0].as<double>(), nc1, X.gcomb[1].as<int32_t>(),
                        c->gpart[1].as<double>(), c->gram[1].as<double>(), GS, GSP, mark, n_ent[0]);
     FIA_HIP_TRY(hipGetLastError());
