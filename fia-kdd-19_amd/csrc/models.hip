@@ -1458,6 +1458,8 @@ constexpr int kRowsRG = FIA_ROWS_RG;      // pivot reads per group (A/B build kn
 template <class M>
 __global__ __launch_bounds__(256) void k_ncf_query_pro(QueryArgs A, int64_t Q, double* __restrict__ qpro) {
   constexpr int K = M::K, H2 = K / 2, Ds = M::Ds, D = M::D, PS = qpro_stride<M>();
+  constexpr int EPL = H2 / 4, GPL = 2 * K / 4, FPL = K / 4;   // per-lane shares of a query's outputs
+  static_assert(H2 % 4 == 0, "k a multiple of 8");
   // the MLP weights as fp64 in LDS, read per use as broadcasts (per-use scalar loads of the
   // fp32 tables expose a memory latency per weight)
   __shared__ double sW1[2 * K * K], sW2[K * H2], sW3[3 * H2], sb1[K], sb2[H2];
@@ -1467,38 +1469,46 @@ __global__ __launch_bounds__(256) void k_ncf_query_pro(QueryArgs A, int64_t Q, d
   for (int e = threadIdx.x; e < K; e += 256) sb1[e] = (double)A.t[5][e];
   for (int e = threadIdx.x; e < H2; e += 256) sb2[e] = (double)A.t[7][e];
   __syncthreads();
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q >= Q) return;
+  // four lanes per query (quad sub = 0..3): each computes a quarter of z2 / g / the gmf terms;
+  // every lane of a quad stays active for the quad exchanges
+  const int sub = threadIdx.x & 3, base = threadIdx.x & 63 & ~3;
+  const int64_t q0 = (int64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const bool qok = q0 < Q;
+  const int64_t q = qok ? q0 : Q - 1;
   const int32_t u = A.qu[q], i = A.qi[q];
   const bool ok = u >= 0 && u < A.U && i >= 0 && i < A.I;
   const int32_t uu = ok ? u : 0, ii = ok ? i : 0;         // clamped ids (n = 0 for invalid ones)
-  const int64_t n = ok ? (A.ptr[0][uu + 1] - A.ptr[0][uu]) + (A.ptr[1][ii + 1] - A.ptr[1][ii]) : 0;
-  double cdup, rsum;
-  A.pairs.lookup((unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii, cdup, rsum);
   const double* __restrict__ l1u = A.l1[0] + (int64_t)uu * K;
   const double* __restrict__ l1i = A.l1[1] + (int64_t)ii * K;
   double z1[K];
 #pragma unroll
   for (int a = 0; a < K; ++a) z1[a] = l1u[a] + l1i[a] + sb1[a];
-  double d2[H2], rh = 0.0;
+  double d2o[EPL], part = 0.0;
 #pragma unroll
-  for (int e = 0; e < H2; ++e) {
+  for (int m = 0; m < EPL; ++m) {                 // hidden unit e = m * 4 + sub
+    const int e = m * 4 + sub;
     double z2 = sb2[e];
 #pragma unroll
     for (int c = 0; c < K; ++c) z2 = fma(sW2[c * H2 + e], z1[c] > 0.0 ? z1[c] : 0.0, z2);
     const bool on = z2 > 0.0;
-    d2[e] = on ? sW3[e] : 0.0;
-    rh += on ? sW3[e] * z2 : 0.0;
+    d2o[m] = on ? sW3[e] : 0.0;
+    part += on ? sW3[e] * z2 : 0.0;
   }
+  double d2[H2];
+#pragma unroll
+  for (int e = 0; e < H2; ++e) d2[e] = __shfl(d2o[e / 4], base + (e & 3));
   double* __restrict__ P = qpro + q * PS;
   const float* __restrict__ pg = A.t[2] + (int64_t)uu * K;
   const float* __restrict__ qg = A.t[3] + (int64_t)ii * K;
 #pragma unroll
-  for (int a = 0; a < K; ++a) {
+  for (int m = 0; m < FPL; ++m) {
+    const int a = m * 4 + sub;
     const double w3g = sW3[H2 + a], pga = (double)pg[a], qga = (double)qg[a];
-    rh += w3g * pga * qga;
-    P[K + a] = w3g * qga;              // d r / d Pg_u = W3g * Qg_i
-    P[Ds + K + a] = w3g * pga;         // d r / d Qg_i = W3g * Pg_u
+    part += w3g * pga * qga;
+    if (qok) {
+      P[K + a] = w3g * qga;            // d r / d Pg_u = W3g * Qg_i
+      P[Ds + K + a] = w3g * pga;       // d r / d Qg_i = W3g * Pg_u
+    }
   }
   double d1[K];
 #pragma unroll
@@ -1509,16 +1519,24 @@ __global__ __launch_bounds__(256) void k_ncf_query_pro(QueryArgs A, int64_t Q, d
     d1[c] = z1[c] > 0.0 ? s : 0.0;
   }
 #pragma unroll
-  for (int a = 0; a < 2 * K; ++a) {    // rows a < K: W1[:k] (user block), a >= K: W1[k:] (item block)
+  for (int m = 0; m < GPL; ++m) {      // rows a < K: W1[:k] (user block), a >= K: W1[k:] (item block)
+    const int a = m * 4 + sub;
     double s = 0.0;
 #pragma unroll
     for (int c = 0; c < K; ++c) s = fma(sW1[a * K + c], d1[c], s);
-    P[a < K ? a : Ds + (a - K)] = s;
+    if (qok) P[a < K ? a : Ds + (a - K)] = s;
   }
-  P[D] = rh + (double)A.t[9][0];
-  P[D + 1] = (double)n;
-  P[D + 2] = cdup;
-  P[D + 3] = 0.0;
+  part += __shfl_xor(part, 1);
+  part += __shfl_xor(part, 2);
+  if (sub == 0 && qok) {
+    const int64_t n = ok ? (A.ptr[0][uu + 1] - A.ptr[0][uu]) + (A.ptr[1][ii + 1] - A.ptr[1][ii]) : 0;
+    double cdup, rsum;
+    A.pairs.lookup((unsigned long long)uu * (unsigned long long)A.I + (unsigned long long)ii, cdup, rsum);
+    P[D] = part + (double)A.t[9][0];
+    P[D + 1] = (double)n;
+    P[D + 2] = cdup;
+    P[D + 3] = 0.0;
+  }
 }
 
 // Step J of k_solve_rows.  P0 / P1: the pivot slots of even / odd steps ([0, 32) the
@@ -3974,7 +3992,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     } else if (pair_layout<M>() && solve_mode() == 0) {
       if constexpr (pair_layout<M>()) {
         FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
-        hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, s, A, Q,
+        hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(256), 0, s, A, Q,
                            c->qwork.as<double>());
         hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
                            (const double*)c->qwork.as<double>(), c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
