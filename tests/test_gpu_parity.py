@@ -423,6 +423,25 @@ def test_mf_item_run_schedule_variant():
     assert " passed" in r.stdout and "deselected" in r.stdout
 
 
+@pytest.mark.parametrize("mode", ["col", "tile", "cols"])
+def test_ncf_side_solve_variants(mode):
+    """The A/B side solves (FIA_SOLVE=col: k_solve_col, tile: k_solve_tile, cols: the
+    one-column-per-lane k_solve) read the NCF k=16 Gram caches in their row-pair layout (gidx)
+    and pass the NCF golden and every-built-size oracle checks.  The knob is read once per
+    process, so the checks run in a child pytest with it set."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, FIA_SOLVE=mode)
+    sel = ("small_golden and ncf or ml1m_rq1_golden and NCF or yelp_ncf_sample or every_built_size and NCF-16 "
+           "or every_built_size and NCF-8")
+    r = subprocess.run([sys.executable, "-m", "pytest", os.path.join(root, "tests", "test_gpu_parity.py"), "-m", "gpu",
+                        "-q", "-x", "-p", "no:cacheprovider", "-k", sel], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and "deselected" in r.stdout
+
+
 @pytest.mark.parametrize("name", ["small_mf_k16.npz", "small_ncf_k16.npz"])
 def test_cached_inverse_hvp_force_refresh_false(name, tmp_path):
     """get_influence_on_test_loss(force_refresh=False) with the reference's cached
