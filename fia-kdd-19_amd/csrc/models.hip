@@ -122,14 +122,56 @@ __device__ __forceinline__ bool better(double a1, int p1, double a2, int p2) {
   return a1 > a2 || (a1 == a2 && p1 < p2);
 }
 
-__device__ __forceinline__ void wave_best(double& a, int& p, double& v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double oa = __shfl_xor(a, off);
-    int op = __shfl_xor(p, off);
-    double ov = __shfl_xor(v, off);
-    if (better(oa, op, a, p)) { a = oa; p = op; v = ov; }
+// The best (key, position, value) of the wave, in every lane.  `better` is a strict total
+// order on (key, position) -- positions are unique, invalid lanes all carry the same
+// (-2, INT_MAX, 0) -- so the result does not depend on the reduction order: DPP row
+// rotations inside each 16-lane row, then permlane swaps across the rows (all VALU; the
+// ds_bpermute butterfly it replaces waited an LDS round trip per level, six per call)
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int x) {
+  // old = x: a disabled source lane returns the lane's own value (a no-op merge)
+  return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ void best_take(double& a, int& p, double& v, double oa, int op, double ov) {
+  if (better(oa, op, a, p)) { a = oa; p = op; v = ov; }
+}
+template <int CTRL>
+__device__ __forceinline__ void best_dpp_step(double& a, int& p, double& v) {
+  const long long ab = __double_as_longlong(a), vb = __double_as_longlong(v);
+  const int alo = dpp_i32<CTRL>((int)(ab & 0xffffffffll)), ahi = dpp_i32<CTRL>((int)(ab >> 32));
+  const int vlo = dpp_i32<CTRL>((int)(vb & 0xffffffffll)), vhi = dpp_i32<CTRL>((int)(vb >> 32));
+  const int op = dpp_i32<CTRL>(p);
+  best_take(a, p, v, __longlong_as_double(((long long)ahi << 32) | (unsigned)alo), op,
+            __longlong_as_double(((long long)vhi << 32) | (unsigned)vlo));
+}
+// the other row of the lane's pair: rows 0<->1, 2<->3 (SW32 = false) or 0,1<->2,3 (SW32 = true)
+template <bool SW32>
+__device__ __forceinline__ unsigned other_rows(unsigned x) {
+  const bool up = SW32 ? (threadIdx.x & 32) != 0 : (threadIdx.x & 16) != 0;
+  if constexpr (SW32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);   // {[r0 r1 r0 r1], [r2 r3 r2 r3]}
+    return up ? r[0] : r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);   // {[r0 r0 r2 r2], [r1 r1 r3 r3]}
+    return up ? r[0] : r[1];
   }
+}
+template <bool SW32>
+__device__ __forceinline__ void best_row_step(double& a, int& p, double& v) {
+  const long long ab = __double_as_longlong(a), vb = __double_as_longlong(v);
+  const unsigned alo = other_rows<SW32>((unsigned)(ab & 0xffffffffll)), ahi = other_rows<SW32>((unsigned)(ab >> 32));
+  const unsigned vlo = other_rows<SW32>((unsigned)(vb & 0xffffffffll)), vhi = other_rows<SW32>((unsigned)(vb >> 32));
+  const int op = (int)other_rows<SW32>((unsigned)p);
+  best_take(a, p, v, __longlong_as_double(((long long)ahi << 32) | alo), op,
+            __longlong_as_double(((long long)vhi << 32) | vlo));
+}
+__device__ __forceinline__ void wave_best(double& a, int& p, double& v) {
+  best_dpp_step<0x128>(a, p, v);   // row_ror:8
+  best_dpp_step<0x124>(a, p, v);   // row_ror:4
+  best_dpp_step<0x122>(a, p, v);   // row_ror:2
+  best_dpp_step<0x121>(a, p, v);   // row_ror:1 -- every lane of a row holds the row's best
+  best_row_step<false>(a, p, v);
+  best_row_step<true>(a, p, v);
 }
 
 // Block-wide K-round selection over per-thread candidate lists (NC each).  Round t
