@@ -3154,6 +3154,20 @@ __device__ __forceinline__ double bcast_row3(double x) {
   return __longlong_as_double(((long long)h16[1] << 32) | l16[1]);
 }
 
+template <int CTRL>
+__device__ __forceinline__ void ikey_dpp_step(long long& k, int& p, double& v) {
+  const long long vb = __double_as_longlong(v);
+  const int klo = dpp_i32<CTRL>((int)(k & 0xffffffffll)), khi = dpp_i32<CTRL>((int)(k >> 32));
+  const int vlo = dpp_i32<CTRL>((int)(vb & 0xffffffffll)), vhi = dpp_i32<CTRL>((int)(vb >> 32));
+  const int p2 = dpp_i32<CTRL>(p);
+  const long long k2 = ((long long)khi << 32) | (unsigned)klo;
+  if (k2 > k || (k2 == k && p2 < p)) {
+    k = k2;
+    p = p2;
+    v = __longlong_as_double(((long long)vhi << 32) | (unsigned)vlo);
+  }
+}
+
 __device__ __forceinline__ long long topk_ikey(double v) {
   // |v|'s bits order like |v| (non-negative doubles); NaN ranks below every number
   const long long b = __double_as_longlong(v) & 0x7fffffffffffffffll;
@@ -3340,13 +3354,12 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         long long k1 = bk[r];
         int p1 = bp[r];
         double v1 = bv[r];
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-          const long long k2 = __shfl_xor(k1, off);
-          const int p2 = __shfl_xor(p1, off);
-          const double v2 = __shfl_xor(v1, off);
-          if (k2 > k1 || (k2 == k1 && p2 < p1)) { k1 = k2; p1 = p2; v1 = v2; }
-        }
+        // the row's best over its 16 lanes by DPP row rotations (order-independent: strict
+        // (key, position) order, unique positions)
+        ikey_dpp_step<0x128>(k1, p1, v1);
+        ikey_dpp_step<0x124>(k1, p1, v1);
+        ikey_dpp_step<0x122>(k1, p1, v1);
+        ikey_dpp_step<0x121>(k1, p1, v1);
         if (cn == 0 && qv[r]) {       // (no loads here: a load in the tile loop drains vmcnt)
           const int64_t slot = (cslot[r] + chunk) * K_top;
           const bool okk = k1 > -2;
