@@ -70,14 +70,17 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 // Every stream-taking entry point starts here.  DevBuf regrows free their old block in
 // order on the CALLING stream; when the caller switches streams, kernels of the previous
-// call may still be queued on the old one, so the device is synchronised first (rare: a
-// context normally sees one stream).  A capturing stream cannot synchronise -- and cannot
-// regrow a buffer either (DevBuf::reserve refuses), so nothing is freed under it.
+// call may still be queued on the old one, so that stream is synchronised first (rare: a
+// context normally sees one stream).  Only the context's own previous stream is waited for
+// -- never the whole device, which would also wait for (and, in global capture mode,
+// invalidate a capture on) other contexts' streams.  A previous stream that is capturing
+// cannot be synchronised; nothing of ours can be freed under it (DevBuf::reserve refuses to
+// regrow during a capture).
 hipError_t enter_stream(fia_ctx* c, hipStream_t s) {
   if (c->has_stream && c->stream != s) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
-      hipError_t e = hipDeviceSynchronize();
+    if (hipStreamIsCapturing(c->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+      hipError_t e = hipStreamSynchronize(c->stream);
       if (e != hipSuccess) return e;
     }
   }
@@ -319,12 +322,12 @@ static int query_batch_common(fia_ctx* c, int64_t Q, const int32_t* qu, const in
     if (Q == 0) return FIA_OK;
     DeviceGuard g(c->device);
     if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
-    const int64_t max_chunks = 2 * Q + total_rel / fia::kChunk + 1;
+    // chunk descriptors / candidate slots: at most 2 per query + one per kRunChunk ratings
+    const int64_t max_chunks = 2 * Q + total_rel / fia::kRunChunk + 1;
     bool unsup = false;
     hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,
                                     topk_idx, topk_val, as_stream(stream), unsup, x_in);
-    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, x_in ? "scoring from a given x is built for the small-k models"
-                                                         : "model/k not supported");
+    if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
     if (e != hipSuccess) return hip_fail(c, e, "fia_query_batch");
     return FIA_OK;
   })

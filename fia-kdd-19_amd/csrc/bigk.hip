@@ -1233,6 +1233,51 @@ __global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __res
   }
 }
 
+// fia_query_batch_x (a given inverse HVP, mf:210-214): the padded solution and this side's
+// record words from x_in (reference theta order) instead of the k_bs_* solve -- the same
+// words k_bs_back / k_big_solve write, from the prologue's theta and v.  One wave per (query, side).
+template <class M>
+__global__ __launch_bounds__(64) void k_big_record_x(BigArgs A, int64_t Q, const double* __restrict__ x_in,
+                                                     const double* __restrict__ qwork, double* __restrict__ xb,
+                                                     double* __restrict__ rec) {
+  constexpr int K = M::K, NPs = M::NPs, Ds = M::Ds, D = 2 * Ds;
+  const int tid = threadIdx.x;
+  for (int64_t w = blockIdx.x; w < 2 * Q; w += gridDim.x) {
+    const int64_t q = w >> 1;
+    const int sd = (int)(w & 1);
+    const double* __restrict__ qw = qwork + q * M::QW;
+    const double* __restrict__ vsd = qw + 8 + sd * NPs;
+    const double* __restrict__ th = qw + 8 + 2 * NPs + sd * NPs;
+    const double* __restrict__ xq = x_in + q * D;
+    double* __restrict__ xo = xb + q * 2 * NPs + sd * NPs;
+    double* __restrict__ R = rec + q * M::R;
+    double* __restrict__ S = R + 8 + sd * M::SB;
+    double cq = 0.0, xv = 0.0;
+    for (int a = tid; a < NPs; a += 64) {
+      const double xa = a < Ds ? xq[M::ref_index(sd, a)] : 0.0;
+      xo[a] = xa;
+      if (a < Ds) {
+        if (M::decayed(a)) cq = fma(xa, th[a], cq);
+        xv = fma(xa, vsd[a], xv);
+      }
+      if constexpr (!M::ncf) {
+        if (a <= K) S[a] = xa;
+      } else {
+        if (a < K) S[a] = xa;
+        else if (a < Ds) S[a] = (double)A.t[8][M::H + (a - K)] * xa;
+      }
+    }
+    cq = wsum(cq);
+    xv = wsum(xv);
+    if (tid == 0) {
+      R[4 + 2 * sd] = A.wd * cq;
+      R[5 + 2 * sd] = xv;
+      const int32_t u = A.qu[q], i = A.qi[q];
+      S[M::ncf ? 2 * K : K + 1] = (double)(sd ? u : i);
+    }
+  }
+}
+
 // per-query record header and x in the reference theta order
 template <class M>
 __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __restrict__ qwork,
@@ -1837,7 +1882,8 @@ hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, c
 template <class M>
 hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                           int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
-                          int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+                          int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
+                          const double* x_in) {
   constexpr int NPs = M::NPs, NPASS = kScoreRows, SW = score_waves<M>();
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * M::QW + 1), s));
@@ -1860,11 +1906,19 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   hipLaunchKernelGGL(k_big_prologue<M>, dim3(grid_cap(Q, 1 << 20)), dim3(256), 0, s, A, Q, c->qwork.as<double>(),
                      c->syslist.as<int32_t>(), c->cpllist.as<int32_t>());
   FIA_HIP_TRY(hipGetLastError());
-  if (!getenv("FIA_BIG_SOLVE_PERSISTENT"))
-    FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
-  else
-    FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
-  FIA_HIP_TRY((launch_solve<M, 2 * NPs, true>(c, A, Q, c->cpllist.as<int32_t>(), s)));
+  if (x_in) {
+    // a given inverse HVP: the records straight from it, no solve (fia_query_batch_x)
+    if (Q > 0)
+      hipLaunchKernelGGL(k_big_record_x<M>, dim3(grid_cap(2 * Q, 1 << 20)), dim3(64), 0, s, A, Q, x_in,
+                         (const double*)c->qwork.as<double>(), c->xb.as<double>(), c->rec.as<double>());
+    FIA_HIP_TRY(hipGetLastError());
+  } else {
+    if (!getenv("FIA_BIG_SOLVE_PERSISTENT"))
+      FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+    else
+      FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+    FIA_HIP_TRY((launch_solve<M, 2 * NPs, true>(c, A, Q, c->cpllist.as<int32_t>(), s)));
+  }
   hipLaunchKernelGGL(k_big_finish<M>, dim3(grid_cap(Q, 1 << 20)), dim3(64), 0, s, Q, c->qwork.as<double>(),
                      c->xb.as<double>(), c->rec.as<double>(), x_out);
   FIA_HIP_TRY(hipGetLastError());
@@ -1937,11 +1991,11 @@ hipError_t check_cover(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
 
 hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                      int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
-                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s) {
+                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s, const double* x_in) {
 #define X(m, kk, T)                                                                                            \
   if (c->p.model == m && c->p.k == kk)                                                                         \
     return query_big_impl<T>(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos, topk_idx, \
-                             topk_val, s);
+                             topk_val, s, x_in);
   FIA_BIG_CASES(X)
 #undef X
   return hipErrorInvalidValue;

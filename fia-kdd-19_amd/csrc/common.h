@@ -15,7 +15,10 @@ constexpr int kWave = 64;
 constexpr int kScoreThreads = 256;       // scoring workgroup (4 independent waves)
 constexpr int kScoreRows = 4;            // related ratings per lane and chunk
 constexpr int kChunk = 64 * kScoreRows;  // related ratings per scoring chunk (one wave)
-constexpr int kRunQB = 16;               // queries per item-run block (k_score_mf_run)
+constexpr int kRunQB = 16;               // queries per item-run block (k_score_mf_runs)
+constexpr int kRunChunk = 128;           // related ratings per item-run descriptor (k_score_mf_runs)
+constexpr int kRunUserCost = 3;          // scheduling cost of a user-side run descriptor (k_score_mf_runs
+                                         // slices): 2 per descriptor + 1 per query of its run
 
 // One scoring chunk: <= kChunk consecutive ratings of ONE side (user list or item
 // list) of one query, so every value a wave needs from the query is wave-uniform.
@@ -194,6 +197,7 @@ struct fia_ctx {
   fia::DevBuf grank;      // int32 [2Q] rank of query q in its user group / item group
   fia::DevBuf gq;         // int32 [2Q] queries grouped by entity (users then items)
   fia::DevBuf qbase;      // int64 [2Q] per query and side: output base, candidate-slot base
+  fia::DevBuf slices;     // int32 [n + 1] first descriptor of each equal-cost slice (k_score_mf_runs)
   fia::DevBuf wstart;     // int64 [U + I + 1] exclusive scan of the work items per entity
   fia::DevBuf gscan;      // k_group_scan tile words + counters (left zero by every launch)
   fia::DevBuf witems;     // int32 [3 * max items] {global entity, list chunk, query block}
@@ -239,11 +243,13 @@ hipError_t count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
                          const int64_t* offsets, int32_t* rel, hipStream_t s);
 // per-query chunk offsets coff (+ chunk descriptors unless offsets_only; with `runs` the
-// descriptors are the compacted work list of k_score_mf_run: every user-side chunk, the
-// item-side chunks of run heads only, their count at qbase[4Q])
+// descriptors are the compacted work list of k_score_mf_runs: every user-side chunk, the
+// item-side chunks of run heads only, their count at qbase[4Q]; and the equal-cost slices of
+// that list, c->slices[0 .. n] with n at qbase[4Q + 1], slice_cost units each -- rounded up
+// to a power of two)
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr,
-                        bool runs = false);
+                        bool runs = false, int slice_cost = 0);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
 int64_t gram_chunk(int64_t want);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
@@ -274,7 +280,14 @@ hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
 hipError_t check_cover(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag, hipStream_t s);
 hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                      int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
-                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s);
+                     int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
+                     const double* x_in = nullptr);
+// MF k <= 16 item-run scoring (score_mf.hip); QueryArgs is in kern.h
+struct QueryArgs;
+hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t Q,
+                                const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
+                                const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
+                                double* cand_val);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,

@@ -140,10 +140,10 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     const int64_t* __restrict__ iptr, int64_t U, int64_t I, int64_t* __restrict__ out,
     unsigned long long* __restrict__ tstate, unsigned int* __restrict__ tctr, int32_t* __restrict__ flag,
     const int64_t* __restrict__ offsets, ChunkDesc* __restrict__ cdesc, int32_t* __restrict__ zero_word,
-    int64_t* __restrict__ qbase, int runs) {
+    int64_t* __restrict__ qbase, int runs, int clen, int lsh, int32_t* __restrict__ slices) {
   __shared__ int s_tile;
-  __shared__ int64_t s_wave[kScanThreads / 64];
-  __shared__ int64_t s_prefix;
+  __shared__ int64_t s_wave[kScanThreads / 64], s_wave2[kScanThreads / 64];
+  __shared__ int64_t s_prefix, s_prefix2;
   const unsigned ntiles = (unsigned)((Q + 1 + kScanTile - 1) / kScanTile);
   if (threadIdx.x == 0) s_tile = (int)atomicAdd(&tctr[0], 1u);
   __syncthreads();
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   // after the look-back, instead of a second dependent qu/qi -> ptr round trip
   int64_t s_ub[kScanItems], s_du[kScanItems], s_ib[kScanItems], s_di[kScanItems], s_base[kScanItems];
   int s_nq[kScanItems];
-  int64_t tsum = 0;
+  int64_t tsum = 0, tsum2 = 0;     // tsum2: runs mode, the descriptors' scheduling cost
 #pragma unroll
   for (int it = 0; it < kScanItems; ++it) {
     const int64_t q = q0 + it;
@@ -171,9 +171,9 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
         s_ub[it] = ub; s_du[it] = du; s_ib[it] = ib; s_di[it] = di;
         x = MODE == 0 ? du + di : (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
         if (MODE == 1 && runs) {
-          // packed {chunks (candidate slots) << 31 | work descriptors}: the item-side chunks
-          // are work only for a run head (first query of a run of equal test items, runs cut
-          // at multiples of kRunQB), which scores them for the whole run
+          // packed {chunks (candidate slots) << 31 | work descriptors}, chunks of clen ratings:
+          // the item-side chunks are work only for a run head (first query of a run of equal
+          // test items, runs cut at multiples of `runs`), which scores them for the whole run
           const bool head = (q % runs) == 0 || qi[q - 1] != i;
           s_nq[it] = 0;
           if (head) {
@@ -185,7 +185,9 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
             }
             s_nq[it] = nq;
           }
-          x = (x << 31) | ((du + kChunk - 1) / kChunk + (head ? (di + kChunk - 1) / kChunk : 0));
+          const int64_t cu = (du + clen - 1) / clen, ci = (di + clen - 1) / clen;
+          x = ((cu + ci) << 31) | (cu + (head ? ci : 0));
+          tsum2 += cu * kRunUserCost + (head ? ci * (s_nq[it] + 2) : 0);
         }
       } else if (MODE == 0) {
         atomicOr(flag + 1, 1);
@@ -201,61 +203,92 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     const int64_t y = __shfl_up(inc, off);
     if (lane >= off) inc += y;
   }
-  if (lane == 63) s_wave[wave] = inc;
+  int64_t inc2 = tsum2;
+  if (MODE == 1 && runs) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(inc2, off);
+      if (lane >= off) inc2 += y;
+    }
+  }
+  if (lane == 63) { s_wave[wave] = inc; s_wave2[wave] = inc2; }
   __syncthreads();
-  int64_t wbase = 0, agg = 0;
+  int64_t wbase = 0, agg = 0, wbase2 = 0, agg2 = 0;
 #pragma unroll
   for (int w = 0; w < kScanThreads / 64; ++w) {
-    if (w < wave) wbase += s_wave[w];
+    if (w < wave) { wbase += s_wave[w]; wbase2 += s_wave2[w]; }
     agg += s_wave[w];
+    agg2 += s_wave2[w];
   }
   if (wave == 0) {
     const int64_t excl = scan_lookback(tstate, tile, agg);
+    // runs mode: the cost prefix on the second tile-word array
+    const int64_t excl2 = (MODE == 1 && runs) ? scan_lookback(tstate + ntiles, tile, agg2) : 0;
     if (lane == 0) {
       s_prefix = excl;
+      s_prefix2 = excl2;
       if (MODE == 1 && tile == 0 && zero_word) zero_word[0] = 0;   // solve's coupled-query counter
     }
   }
   __syncthreads();
   int64_t run = s_prefix + wbase + inc - tsum;
+  int64_t run2 = s_prefix2 + wbase2 + inc2 - tsum2;    // cost prefix of this thread's first query
   constexpr int64_t kLo = (1ll << 31) - 1;
 #pragma unroll
   for (int it = 0; it < kScanItems; ++it) {
     const int64_t q = q0 + it;
     if (q <= Q) out[q] = (MODE == 1 && runs) ? run >> 31 : run;
-    if (MODE == 1 && runs && q == Q) qbase[4 * Q] = run & kLo;     // work descriptors in all
+    if (MODE == 1 && runs && q == Q) {
+      // work descriptors in all; slices in all (cost run2 in slices of lam) and the end mark
+      const int64_t nw = run & kLo, ns = (run2 + (1ll << lsh) - 1) >> lsh;
+      qbase[4 * Q] = nw;
+      qbase[4 * Q + 1] = ns;
+      if (slices) slices[ns] = (int32_t)nw;
+    }
     if (MODE == 1 && qbase && q < Q) {
       // per query: {out base user, item}, {candidate slot base user, item} (k_score_mf_run)
       const int64_t du = s_du[it], cr = runs ? run >> 31 : run;
       qbase[4 * q + 0] = s_base[it];
       qbase[4 * q + 1] = s_base[it] + du;
       qbase[4 * q + 2] = cr;
-      qbase[4 * q + 3] = cr + (du + kChunk - 1) / kChunk;
+      qbase[4 * q + 3] = cr + (du + (runs ? clen : kChunk) - 1) / (runs ? clen : kChunk);
     }
     if (MODE == 1 && runs && cdesc && q < Q && v[it] > 0) {
       const int64_t ub = s_ub[it], du = s_du[it], ib = s_ib[it], di = s_di[it];
       int64_t c = run & kLo;
       const int64_t base = s_base[it];
-      for (int64_t st = 0; st < du; st += kChunk, ++c) {
+      // descriptor c with cost w at cost prefix p starts every slice whose start point
+      // s * lam lies in [p, p + w) (slices of a descriptor costing more than lam but the
+      // last are empty): every descriptor lands in exactly one slice
+      // (lam = 1 << lsh: shifts, no 64-bit division in this per-descriptor loop)
+      int64_t p = run2;
+      auto mark = [&](int64_t cd, int64_t w) {
+        if (slices)
+          for (int64_t sl = (p + (1ll << lsh) - 1) >> lsh; (sl << lsh) < p + w; ++sl) slices[sl] = (int32_t)cd;
+        p += w;
+      };
+      for (int64_t st = 0; st < du; st += clen, ++c) {
         ChunkDesc d;
         d.list_base = ub + st;
         d.out_base = base + st;
         d.q = (int32_t)q;
         d.pos0 = (int32_t)st;
-        d.len = (int32_t)(du - st < kChunk ? du - st : kChunk);
+        d.len = (int32_t)(du - st < clen ? du - st : clen);
         d.side = 0 | (1 << 8);
         cdesc[c] = d;
+        mark(c, kRunUserCost);
       }
       if (s_nq[it] > 0)
-        for (int64_t st = 0; st < di; st += kChunk, ++c) {
+        for (int64_t st = 0; st < di; st += clen, ++c) {
           ChunkDesc d;
           d.list_base = ib + st;
           d.out_base = base + du + st;
           d.q = (int32_t)q;
           d.pos0 = (int32_t)(du + st);
-          d.len = (int32_t)(di - st < kChunk ? di - st : kChunk);
+          d.len = (int32_t)(di - st < clen ? di - st : clen);
           d.side = 1 | (s_nq[it] << 8);
           cdesc[c] = d;
+          mark(c, s_nq[it] + 2);
         }
     } else
     if (MODE == 1 && cdesc && q < Q && v[it] > 0) {
@@ -284,6 +317,10 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
       }
     }
     run += v[it];
+    if (MODE == 1 && runs && q < Q && v[it] > 0) {
+      const int64_t cu = (s_du[it] + clen - 1) / clen, ci = (s_di[it] + clen - 1) / clen;
+      run2 += cu * kRunUserCost + (s_nq[it] > 0 ? ci * (s_nq[it] + 2) : 0);
+    }
   }
   // the last tile to finish resets the tile words and the counters for the next launch
   __syncthreads();
@@ -294,7 +331,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned done = atomicAdd(&tctr[1], 1u);
     if (done == ntiles - 1) {
-      for (unsigned t = 0; t < ntiles; ++t)
+      for (unsigned t = 0; t < (MODE == 1 && runs ? 2 * ntiles : ntiles); ++t)
         __hip_atomic_store(&tstate[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&tctr[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&tctr[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -602,7 +639,7 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
 // them zero again
 static hipError_t scan_state(fia_ctx* c, int64_t Q, hipStream_t s) {
   const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
-  const size_t need = sizeof(unsigned long long) * (size_t)ntiles + 16;
+  const size_t need = sizeof(unsigned long long) * (size_t)(2 * ntiles) + 16;   // two tile-word arrays (runs)
   if (c->qscan.bytes >= need && c->qscan.ptr) return hipSuccess;
   // stream-ordered regrow (the previous launches on s still own the old block)
   FIA_HIP_TRY(c->qscan.reserve(need < 4096 ? 4096 : need, s));
@@ -613,14 +650,16 @@ static hipError_t scan_state(fia_ctx* c, int64_t Q, hipStream_t s) {
 template <int MODE>
 static hipError_t launch_query_scan(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int64_t* out,
                                     const int64_t* offsets, ChunkDesc* cdesc, int32_t* zero_word, hipStream_t s,
-                                    int64_t* qbase = nullptr, int runs = 0) {
+                                    int64_t* qbase = nullptr, int runs = 0, int clen = kChunk, int lsh = 0,
+                                    int32_t* slices = nullptr) {
   FIA_HIP_TRY(scan_state(c, Q, s));
   FIA_HIP_TRY(c->flag.reserve(64, s));
   const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
   unsigned int* ctr = reinterpret_cast<unsigned int*>(c->qscan.as<char>() + c->qscan.bytes - 16);
   hipLaunchKernelGGL(k_query_scan<MODE>, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, qu, qi, Q,
                      c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I, out,
-                     c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word, qbase, runs);
+                     c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word, qbase, runs,
+                     clen, lsh, slices);
   return hipGetLastError();
 }
 
@@ -640,19 +679,28 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 
 // queries per item-run block (A/B knob FIA_RUN_QB, 1 = no sharing)
 static int run_qb() {
-  static const int v = getenv("FIA_RUN_QB") ? atoi(getenv("FIA_RUN_QB")) : 4;
+  static const int v = getenv("FIA_RUN_QB") ? atoi(getenv("FIA_RUN_QB")) : kRunQB;
   return v < 1 ? 1 : v > kRunQB ? kRunQB : v;
 }
 
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
-                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word, bool runs) {
+                        int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word, bool runs,
+                        int slice_cost) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1), s));
   const bool rq = runs && !offsets_only;
   if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
-  if (rq) FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 1), s));
+  int lsh = 0;                                   // slice cost: the power of two >= slice_cost
+  while ((1 << lsh) < slice_cost && lsh < 30) ++lsh;
+  const int lam = 1 << lsh;
+  if (rq) {
+    FIA_HIP_TRY(c->qbase.reserve(sizeof(int64_t) * (size_t)(4 * Q + 2), s));
+    // total cost <= (kRunQB + 2) per descriptor
+    FIA_HIP_TRY(c->slices.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * (kRunQB + 2) / lam + 2), s));
+  }
   return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
                               offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s,
-                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? run_qb() : 0);
+                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? run_qb() : 0, rq ? kRunChunk : kChunk, lsh,
+                              rq ? c->slices.as<int32_t>() : nullptr);
 }
 
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,

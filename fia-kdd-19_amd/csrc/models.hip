@@ -19,218 +19,10 @@
 #include <cstring>
 #include <type_traits>
 
-#include "common.h"
+#include "kern.h"
 
 namespace fia {
 namespace {
-
-// ------------------------------------------------------------------------------------
-// model traits
-// ------------------------------------------------------------------------------------
-template <int K_>
-struct MFm {
-  static constexpr int K = K_;
-  static constexpr int Ds = K + 1;
-  static constexpr int D = 2 * Ds;
-  static constexpr int SB = 2 * K + 4;          // per-side record: a, xs, bias, xsb, dup_other, pad
-                                                // (even: x_s starts 16-B aligned for k_score_mf_mfma)
-  static constexpr int R = 4 + 2 * SB;          // header: inv_n, c_q, x.v, r-hat(u,i)
-  static constexpr bool ncf = false;
-  __device__ static bool decayed(int a) { return a < K; }
-  // reference theta order [p_u, q_i, b_u, b_i]
-  __device__ static int ref_index(int a) {
-    int side = a >= Ds, j = side ? a - Ds : a;
-    return j < K ? side * K + j : 2 * K + side;
-  }
-};
-
-template <int K_>
-struct NCFm {
-  static constexpr int K = K_;
-  static constexpr int H2 = K / 2;
-  static constexpr int Ds = 2 * K;
-  static constexpr int D = 2 * Ds;
-  static constexpr int SB = 2 * K + 1;          // per-side record: x_mlp, W3g * x_gmf, dup_other
-  static constexpr int R = 4 + 2 * SB;          // header: inv_n, c_q, x.v, r-hat(u,i)
-  static constexpr bool ncf = true;
-  __device__ static bool decayed(int) { return true; }
-  // reference theta order [Pm_u, Qm_i, Pg_u, Qg_i]
-  __device__ static int ref_index(int a) {
-    int side = a >= Ds, j = side ? a - Ds : a;
-    return j < K ? side * K + j : 2 * K + side * K + (j - K);
-  }
-};
-
-__device__ __forceinline__ int tri(int r, int c) { return (r * (r + 1)) / 2 + c; }
-
-// Gram cache element (R >= C) of one side block.  Packed lower triangle, except NCF k = 16
-// (Ds = 32), kept in the row-pair layout of k_solve_rows: lane t of a side system owns rows t
-// and 31 - t, slot C of row t and slot 32 - C of row 31 - t (33 slots per lane), element
-// slot * 16 + t -- one slot of the system's 16 lanes is one 128-B line.
-template <class M>
-__device__ __forceinline__ int gidx(int R, int C) {
-  if constexpr (M::ncf && M::Ds == 32) return R < 16 ? C * 16 + R : (32 - C) * 16 + (31 - R);
-  else return tri(R, C);
-}
-template <class M>
-constexpr bool pair_layout() { return M::ncf && M::Ds == 32; }
-// NCF k <= 16: per list position the Gram pass stores the two ReLU masks of the MLP (bits
-// [0, k) z1 > 0, [k, 3k/2) z2 > 0: 4 B) instead of g_mlp (8k B); scoring rebuilds
-// d1 = 1[z1 > 0] (W2 (1[z2 > 0] W3m)) from a 2^(k/2)-row LDS table and dots it with
-// y = W1_side^T x_mlp (the record's MLP block after k_ncf_rec_y), since
-// x_mlp . g_mlp = x_mlp . (W1_side d1) = (W1_side^T x_mlp) . d1
-template <class M>
-constexpr bool mask_path() { return M::ncf && M::K <= 16; }
-
-// 4 doubles per lane: an f64 MFMA 16x16 tile (C/D layout: element (4 r + (l >> 4), l & 15) in [r])
-typedef double d4_t __attribute__((ext_vector_type(4)));
-
-// lane l's double, broadcast to the wave (v_readlane into SGPRs; l compile-time)
-__device__ __forceinline__ double readlane_d(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-template <int N>
-__device__ __forceinline__ void load_row_f32(const float* __restrict__ src, double* dst) {
-  if constexpr (N % 4 == 0) {
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-#pragma unroll
-    for (int c = 0; c < N / 4; ++c) {
-      float4 t = s4[c];
-      dst[4 * c + 0] = t.x;
-      dst[4 * c + 1] = t.y;
-      dst[4 * c + 2] = t.z;
-      dst[4 * c + 3] = t.w;
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < N; ++c) dst[c] = src[c];
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// top-K helpers: order = |v| descending, then related position ascending
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ double topk_key(double v) {
-  double a = fabs(v);
-  return (a != a) ? -1.0 : a;     // NaN ranks last among real candidates
-}
-__device__ __forceinline__ bool better(double a1, int p1, double a2, int p2) {
-  return a1 > a2 || (a1 == a2 && p1 < p2);
-}
-
-// The best (key, position, value) of the wave, in every lane.  `better` is a strict total
-// order on (key, position) -- positions are unique, invalid lanes all carry the same
-// (-2, INT_MAX, 0) -- so the result does not depend on the reduction order: DPP row
-// rotations inside each 16-lane row, then permlane swaps across the rows (all VALU; the
-// ds_bpermute butterfly it replaces waited an LDS round trip per level, six per call)
-template <int CTRL>
-__device__ __forceinline__ int dpp_i32(int x) {
-  // old = x: a disabled source lane returns the lane's own value (a no-op merge)
-  return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xf, 0xf, false);
-}
-__device__ __forceinline__ void best_take(double& a, int& p, double& v, double oa, int op, double ov) {
-  if (better(oa, op, a, p)) { a = oa; p = op; v = ov; }
-}
-template <int CTRL>
-__device__ __forceinline__ void best_dpp_step(double& a, int& p, double& v) {
-  const long long ab = __double_as_longlong(a), vb = __double_as_longlong(v);
-  const int alo = dpp_i32<CTRL>((int)(ab & 0xffffffffll)), ahi = dpp_i32<CTRL>((int)(ab >> 32));
-  const int vlo = dpp_i32<CTRL>((int)(vb & 0xffffffffll)), vhi = dpp_i32<CTRL>((int)(vb >> 32));
-  const int op = dpp_i32<CTRL>(p);
-  best_take(a, p, v, __longlong_as_double(((long long)ahi << 32) | (unsigned)alo), op,
-            __longlong_as_double(((long long)vhi << 32) | (unsigned)vlo));
-}
-// the other row of the lane's pair: rows 0<->1, 2<->3 (SW32 = false) or 0,1<->2,3 (SW32 = true)
-template <bool SW32>
-__device__ __forceinline__ unsigned other_rows(unsigned x) {
-  const bool up = SW32 ? (threadIdx.x & 32) != 0 : (threadIdx.x & 16) != 0;
-  if constexpr (SW32) {
-    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);   // {[r0 r1 r0 r1], [r2 r3 r2 r3]}
-    return up ? r[0] : r[1];
-  } else {
-    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);   // {[r0 r0 r2 r2], [r1 r1 r3 r3]}
-    return up ? r[0] : r[1];
-  }
-}
-template <bool SW32>
-__device__ __forceinline__ void best_row_step(double& a, int& p, double& v) {
-  const long long ab = __double_as_longlong(a), vb = __double_as_longlong(v);
-  const unsigned alo = other_rows<SW32>((unsigned)(ab & 0xffffffffll)), ahi = other_rows<SW32>((unsigned)(ab >> 32));
-  const unsigned vlo = other_rows<SW32>((unsigned)(vb & 0xffffffffll)), vhi = other_rows<SW32>((unsigned)(vb >> 32));
-  const int op = (int)other_rows<SW32>((unsigned)p);
-  best_take(a, p, v, __longlong_as_double(((long long)ahi << 32) | alo), op,
-            __longlong_as_double(((long long)vhi << 32) | vlo));
-}
-__device__ __forceinline__ void wave_best(double& a, int& p, double& v) {
-  best_dpp_step<0x128>(a, p, v);   // row_ror:8
-  best_dpp_step<0x124>(a, p, v);   // row_ror:4
-  best_dpp_step<0x122>(a, p, v);   // row_ror:2
-  best_dpp_step<0x121>(a, p, v);   // row_ror:1 -- every lane of a row holds the row's best
-  best_row_step<false>(a, p, v);
-  best_row_step<true>(a, p, v);
-}
-
-// Block-wide K-round selection over per-thread candidate lists (NC each).  Round t
-// takes the best candidate strictly worse than round t-1's winner, so no
-// "taken" marks are needed (positions are unique).  Writes K (pos, val) pairs.
-template <int NC, int NT>
-__device__ void block_topk(const double (&ca)[NC], const int (&cp)[NC], const double (&cv)[NC], int K,
-                           int32_t* __restrict__ out_pos, double* __restrict__ out_val, double* s_a, int* s_p,
-                           double* s_v) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int NW = NT / 64;
-  double pa = INFINITY;
-  int pp = -1;
-  for (int t = 0; t < K; ++t) {
-    double ba = -2.0, bv = 0.0;
-    int bp = 0x7fffffff;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      if (cp[c] >= 0 && better(pa, pp, ca[c], cp[c]) && better(ca[c], cp[c], ba, bp)) {
-        ba = ca[c]; bp = cp[c]; bv = cv[c];
-      }
-    }
-    wave_best(ba, bp, bv);
-    if (NW > 1) {
-      if (lane == 0) { s_a[wave] = ba; s_p[wave] = bp; s_v[wave] = bv; }
-      __syncthreads();
-      ba = s_a[0]; bp = s_p[0]; bv = s_v[0];
-#pragma unroll
-      for (int w = 1; w < NW; ++w)
-        if (better(s_a[w], s_p[w], ba, bp)) { ba = s_a[w]; bp = s_p[w]; bv = s_v[w]; }
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      bool ok = ba > -1.5;
-      out_pos[t] = ok ? bp : -1;
-      out_val[t] = ok ? bv : NAN;
-    }
-    pa = ba; pp = bp;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// NCF helpers (NCF.py:85-145): z1 = L1_self + L1_other + b1 given; returns r-hat
-// pieces via the per-row MLP with the ReLU derivative 1[z > 0] (TF ReluGrad).
-// ------------------------------------------------------------------------------------
-template <int K>
-struct NCFWeights {   // LDS copies (fp64)
-  double W2[K * (K / 2)];   // [k][k/2]
-  double b2[K / 2];
-  double W3[3 * (K / 2)];   // [W3m (k/2) ; W3g (k)]
-};
-
-template <int K>
-__device__ void load_ncf_weights(NCFWeights<K>& w, const float* W2, const float* b2, const float* W3) {
-  constexpr int H = K / 2;
-  for (int t = threadIdx.x; t < K * H; t += blockDim.x) w.W2[t] = W2[t];
-  for (int t = threadIdx.x; t < H; t += blockDim.x) w.b2[t] = b2[t];
-  for (int t = threadIdx.x; t < 3 * H; t += blockDim.x) w.W3[t] = W3[t];
-}
 
 // ------------------------------------------------------------------------------------
 // NCF layer-1 halves: L1[0][u] = Pm_u W1[:k], L1[1][i] = Qm_i W1[k:]  (fp64)
@@ -365,11 +157,6 @@ __device__ __forceinline__ double bcast_col(double x, int j) {
   }
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <class M>
 __device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* __restrict__ Gi, double s2n,
@@ -478,26 +265,6 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
-struct QueryArgs {
-  const int32_t* qu;
-  const int32_t* qi;
-  int64_t U, I;
-  const int64_t* ptr[2];
-  const int32_t* row[2];
-  const int32_t* other[2];
-  const float* rating[2];
-  const double* gram[2];
-  const double* l1[2];
-  const float* t[10];
-  double wd, damping;
-  PairTable pairs;
-  // NCF, per list position of each side (written by k_gram_ncf_mfma):
-  // g_mlp,j = W1_side . d1_j coordinate-major [k][N], and e_j = r-hat_j - y_j [side][N]
-  const double* lgm[2];
-  const double* lres;
-  int64_t N;
-  const double* d1tab;   // NCF k <= 16: d1 table [2^(k/2)][k] (k_ncf_d1_table)
-};
 
 // theta_t, v = d r(u,i)/d theta_t (gnn:155, mf:194,201 / ncf:222,229) and r-hat(u,i) of one
 // query into the workgroup's LDS arrays th[D] / g[D] (NTH threads cooperate; r-hat is
@@ -1914,13 +1681,6 @@ struct GramSides {
   const double* lgm[2];
   const float* W3;
   int64_t N;
-  // MF residual pass (k_gram_mf_mfma): e_p = r-hat_p - y_p per list position -> lres[side][N]
-  const float* emb_self[2];
-  const float* bias_self[2];
-  const float* bias_other[2];
-  const float* rating[2];
-  const float* gbias;
-  double* lres;
   // fia_prepare_for (small k): only the entities marked here (users [0, U), items [U, U+I))
   // get their Gram caches / per-position rows; nullptr = every entity
   const uint8_t* mark;
@@ -1928,69 +1688,6 @@ struct GramSides {
   __device__ bool skip(int sd, int32_t e) const { return mark && !mark[moff[sd] + e]; }
 };
 
-
-// MF residual per list position of a Gram work item's slice (k_resid_list_mf: a wave per
-// item right after the Gram pass, so the other-side rows come from L2):
-// e_p = theta_e . g_p + (b_e + g) + b_o - y, summed in the order the per-(rating, query)
-// scoring dots used -> lres[side][N] for k_score_mf_run
-template <class M>
-__device__ __forceinline__ void resid_slice(const GramSides& GSd, int sd, int32_t e, int32_t start, int32_t len,
-                                            int lane) {
-  constexpr int K = M::K;
-  const float* __restrict__ Es = GSd.emb_self[sd] + (int64_t)e * K;
-  const float* __restrict__ emb_other = GSd.emb_other[sd];
-  const double bsg = (double)GSd.bias_self[sd][e] + (double)GSd.gbias[0];
-  const float* __restrict__ bo = GSd.bias_other[sd];
-  const int64_t lb = GSd.ptr[sd][e] + start;
-  const float* __restrict__ rat = GSd.rating[sd] + lb;
-  const int32_t* __restrict__ oth = GSd.other[sd] + lb;
-  double* __restrict__ lr = GSd.lres + (int64_t)sd * GSd.N + lb;
-  // 4 positions per lane per round, every load of the round issued before the first use
-  // (a Gram item is <= 256 positions at k <= 16: one round)
-  constexpr int PR = 4;
-  for (int p0 = 0; p0 < len; p0 += 64 * PR) {
-    int32_t o[PR];
-    float y[PR], bb[PR];
-    float4 t[PR][K / 4];
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      const int p = p0 + 64 * r + lane;
-      const int pc = p < len ? p : 0;
-      o[r] = oth[pc];
-      y[r] = rat[pc];
-    }
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      const float4* row = reinterpret_cast<const float4*>(emb_other + (int64_t)o[r] * K);
-#pragma unroll
-      for (int c4 = 0; c4 < K / 4; ++c4) t[r][c4] = row[c4];
-      bb[r] = bo[o[r]];
-    }
-#pragma unroll
-    for (int r = 0; r < PR; ++r) {
-      double dot = 0.0;
-#pragma unroll
-      for (int c4 = 0; c4 < K / 4; ++c4) {
-        dot = fma((double)Es[4 * c4 + 0], (double)t[r][c4].x, dot);
-        dot = fma((double)Es[4 * c4 + 1], (double)t[r][c4].y, dot);
-        dot = fma((double)Es[4 * c4 + 2], (double)t[r][c4].z, dot);
-        dot = fma((double)Es[4 * c4 + 3], (double)t[r][c4].w, dot);
-      }
-      const int p = p0 + 64 * r + lane;
-      if (p < len) lr[p] = dot + bsg + (double)bb[r] - (double)y[r];
-    }
-  }
-}
-
-template <class M>
-__global__ __launch_bounds__(64) void k_resid_list_mf(GramSides GSd) {
-  const int sd = (int64_t)blockIdx.x >= GSd.n_items[0] ? 1 : 0;
-  const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
-  if (w >= GSd.n_items[sd]) return;
-  const int32_t* __restrict__ items = GSd.items[sd];
-  if (GSd.skip(sd, items[4 * w])) return;
-  resid_slice<M>(GSd, sd, items[4 * w], items[4 * w + 1], items[4 * w + 2], threadIdx.x);
-}
 
 template <class M>
 __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
@@ -2365,216 +2062,11 @@ __global__ __launch_bounds__(256) void k_gram_combine(int64_t n_comb0, const int
 }
 
 // ------------------------------------------------------------------------------------
-// Scoring (the dominant, HBM-streaming kernel), MF per-query chunks: one WAVE per chunk
-// of <= kChunk consecutive ratings of one side of one query.  Per rating j:
+// Scoring (the dominant, HBM-streaming kernel).  Per related rating j of a query:
 //   influence_j = (2 e_j s_j + c_q) / n,  s_j = x . g_j,  e_j = r-hat_j - y_j
-// (mf:240-246: x . grad L_j / n with grad L_j = 2 e_j g_j + wd * M * theta_t); the
-// chunk's K best (|influence| desc, position asc) go to its candidate slots.
-// Software-pipelined across the wave's chunks: a chunk's critical path is three
-// dependent round trips (descriptor -> list entries + record -> gathered rows); the next
-// chunk's descriptor, list entries and record words are loaded while the current
-// chunk's gathers are in flight, so each chunk waits on one round trip.
+// (mf:240-246: x . grad L_j / n with grad L_j = 2 e_j g_j + wd * M * theta_t); the K best
+// of every chunk (|influence| desc, position asc) go to its candidate slots.
 // ------------------------------------------------------------------------------------
-// k_score_mf_run (MF k <= 16, opt-in via FIA_MF_SCORE=run; k_score_mf is the default headline
-// kernel): the per-query chunks of k_score_mf,
-// except that an item-side chunk is scored ONCE for a run of consecutive batch queries
-// with the same test item (<= kRunQB, runs cut at multiples of kRunQB): the run's first
-// query ("head") gathers the chunk's other-side rows once and scores every query of the
-// run; the other queries' item-side descriptors are skipped.  A batch in item-major
-// order (the usual way to answer a test set) shares each popular item's list this way
-// without any group build; any order stays correct (runs of one).  Random 64-B row
-// gathers from the L2-resident tables are what bound the per-query kernel (tools/
-// mb_score.hip: 54 us without them vs 105 us with them at ml-1m-ex), so they are cut
-// to one per (rating, run).  Per chunk: e_j from the Gram pass's residual (A.lres), the
-// run's per-query words (x, 1/n, c_q, x_bias, the dup other, output / slot bases) by one
-// vector load round trip, lane (a, j) holding coordinates 4a..4a+3 of query j, then
-// broadcast per query by v_readlane as SGPR operands.
-//   influence_jq = (2 e_j (x_q . g_j + x_bias,q) + c_q) / n_q          (mf:237-246)
-
-template <class M>
-__global__ __launch_bounds__(kScoreThreads) void k_score_mf_run(
-    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
-    const int64_t* __restrict__ qbase, const double* __restrict__ rec, int32_t* __restrict__ rel_idx,
-    double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf && M::K <= 16 && M::K % 4 == 0, "MF k in {8, 16}");
-  constexpr int K = M::K, RT = kScoreRows, NA = K / 4;
-  const int lane = threadIdx.x & 63, jl = lane & 15, al = lane >> 4;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nwork = qbase[4 * Q];            // compacted work descriptors (build_chunks runs)
-  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  for (int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; ch < nwork; ch += stride) {
-    const ChunkDesc d = cdesc[ch];
-    const int sd = d.side & 0xff, nq = d.side >> 8;
-    const int32_t q = d.q;
-    const int32_t qj = q + (jl < nq ? jl : nq - 1);
-    // list entries of the chunk (positions past its end clamped to its first entry)
-    int32_t o[RT], row[RT];
-    double e[RT];
-    {
-      const int32_t* __restrict__ oth = A.other[sd] + d.list_base;
-      const int32_t* __restrict__ rw = A.row[sd] + d.list_base;
-      const double* __restrict__ res = A.lres + (int64_t)sd * A.N + d.list_base;
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const int idx = r * 64 + lane;
-        const int li = idx < d.len ? idx : 0;
-        o[r] = oth[li];
-        row[r] = rw[li];
-        e[r] = res[li];
-      }
-    }
-    // the run's per-query words: lane (a, j) = query q + j (clamped), coordinates 4a..4a+3
-    double xa[4];
-    double inv_n, cq, xsb;
-    int32_t dupo;
-    int64_t obj, cbj, pbj;
-    {
-      const double* __restrict__ Rj = rec + (int64_t)qj * M::R;
-      const double* __restrict__ Sj = Rj + 4 + sd * M::SB;
-      const int a = al < NA ? al : NA - 1;
-      const double2* xs = reinterpret_cast<const double2*>(Sj + K + 4 * a);
-      const double2 x01 = xs[0], x23 = xs[1];
-      xa[0] = x01.x; xa[1] = x01.y; xa[2] = x23.x; xa[3] = x23.y;
-      inv_n = Rj[0];
-      cq = Rj[1];
-      xsb = Sj[2 * K + 1];
-      dupo = (int32_t)Sj[2 * K + 2];
-      const longlong2* qb = reinterpret_cast<const longlong2*>(qbase + 4 * (int64_t)qj);
-      const longlong2 q01 = qb[0], q23 = qb[1];
-      obj = sd ? q01.y : q01.x;
-      cbj = sd ? q23.y : q23.x;
-      pbj = sd ? q01.y - q01.x : 0;
-    }
-    float g[RT][K];
-    {
-      const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o[r] * K);
-#pragma unroll
-        for (int c = 0; c < NA; ++c) {
-          const float4 t = src[c];
-          g[r][4 * c] = t.x; g[r][4 * c + 1] = t.y; g[r][4 * c + 2] = t.z; g[r][4 * c + 3] = t.w;
-        }
-      }
-    }
-    const int64_t ob0 = ((int64_t)__builtin_amdgcn_readlane((int)(obj >> 32), 0) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((int)(obj & 0xffffffff), 0);
-    const int64_t co = d.out_base - ob0;     // chunk offset inside the side segment (x kChunk)
-    // every load the query loop reads is consumed here: at the loop header hipcc cannot
-    // tell a pending load from the loop's own stores and would wait vmcnt(0) -- for the
-    // previous query's stores -- on every iteration
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      asm volatile("" ::"v"(o[r]), "v"(row[r]), "v"(e[r]));
-#pragma unroll
-      for (int c = 0; c < K; ++c) asm volatile("" ::"v"(g[r][c]));
-    }
-    asm volatile("" ::"v"(xa[0]), "v"(xa[1]), "v"(xa[2]), "v"(xa[3]), "v"(inv_n), "v"(cq), "v"(xsb), "v"(dupo));
-    asm volatile("" ::"v"(obj), "v"(cbj), "v"(pbj));
-    for (int j = 0; j < nq; ++j) {
-      double s[RT];
-      {
-#pragma unroll
-        for (int r = 0; r < RT; ++r) s[r] = 0.0;
-#pragma unroll
-        for (int c4 = 0; c4 < NA; ++c4) {
-#pragma unroll
-          for (int r = 0; r < RT; ++r)
-            asm volatile("" : "+v"(g[r][4 * c4]), "+v"(g[r][4 * c4 + 1]), "+v"(g[r][4 * c4 + 2]),
-                         "+v"(g[r][4 * c4 + 3]), "+v"(s[r]));
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            const double xc = readlane_d(xa[cc], 16 * c4 + j);
-#pragma unroll
-            for (int r = 0; r < RT; ++r) s[r] = fma(xc, (double)g[r][4 * c4 + cc], s[r]);
-          }
-        }
-      }
-      const double inv_nj = readlane_d(inv_n, j), cqj = readlane_d(cq, j), xsbj = readlane_d(xsb, j);
-      const int32_t dupj = __builtin_amdgcn_readlane(dupo, j);
-      const int64_t ob = ((int64_t)__builtin_amdgcn_readlane((int)(obj >> 32), j) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)(obj & 0xffffffff), j);
-      const int64_t cb = ((int64_t)__builtin_amdgcn_readlane((int)(cbj >> 32), j) << 32) |
-                         (uint32_t)__builtin_amdgcn_readlane((int)(cbj & 0xffffffff), j);
-      const int32_t pb = __builtin_amdgcn_readlane((int)pbj, j);
-      double infl[RT];
-      bool dup[RT];
-      bool anyd = false;
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        dup[r] = o[r] == dupj && r * 64 + lane < d.len;
-        anyd = anyd || dup[r];
-        infl[r] = (2.0 * e[r] * (s[r] + xsbj) + cqj) * inv_nj;
-      }
-      if (__builtin_expect(__ballot(anyd) != 0, 0)) {
-        // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
-        const double* __restrict__ R = rec + (int64_t)(q + j) * M::R;
-        const double xv = R[2], rhat_ui = R[3];
-        const float* __restrict__ rat = A.rating[sd] + d.list_base;
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          if (dup[r]) infl[r] = (2.0 * (rhat_ui - (double)rat[r * 64 + lane]) * xv + cqj) * inv_nj;
-      }
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const int idx = r * 64 + lane;
-        if (idx < d.len) {
-          if (influence) __builtin_nontemporal_store(infl[r], influence + ob + co + idx);
-          if (rel_idx) __builtin_nontemporal_store(row[r], rel_idx + ob + co + idx);
-        }
-      }
-      if (K_top == 1) {
-        // running best over the lane's rows (positions ascend with r), then over the wave
-        double ba = -2.0, bv = 0.0;
-        int bp = 0x7fffffff;
-#pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          const int idx = r * 64 + lane;
-          const double key = idx < d.len ? topk_key(infl[r]) : -2.0;
-          if (key > ba) { ba = key; bp = (int)(pb + co) + idx; bv = infl[r]; }
-        }
-        wave_best(ba, bp, bv);
-        if (lane == 0) {
-          const int64_t slot = cb + co / kChunk;
-          const bool okk = ba > -1.5;
-          cand_pos[slot] = okk ? bp : -1;
-          cand_val[slot] = okk ? bv : NAN;
-        }
-      } else if (K_top > 1) {
-        double ca[RT];
-        int cp[RT];
-#pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          const int idx = r * 64 + lane;
-          const bool ok = idx < d.len;
-          cp[r] = ok ? (int)(pb + co) + idx : -1;
-          ca[r] = ok ? topk_key(infl[r]) : -2.0;
-        }
-        const int64_t slot = cb + co / kChunk;
-        double pa = INFINITY;
-        int pp = -1;
-        for (int t = 0; t < K_top; ++t) {
-          double ba = -2.0, bv = 0.0;
-          int bp = 0x7fffffff;
-#pragma unroll
-          for (int r = 0; r < RT; ++r)
-            if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
-              ba = ca[r]; bp = cp[r]; bv = infl[r];
-            }
-          wave_best(ba, bp, bv);
-          if (lane == 0) {
-            const bool okk = ba > -1.5;
-            cand_pos[slot * K_top + t] = okk ? bp : -1;
-            cand_val[slot * K_top + t] = okk ? bv : NAN;
-          }
-          pa = ba;
-          pp = bp;
-        }
-      }
-    }
-  }
-}
 
 // waves per SIMD the headline kernel is compiled for (A/B: -DFIA_SCORE_WAVES=5 spills 68 B/lane)
 #ifndef FIA_SCORE_WAVES
@@ -3180,7 +2672,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
+  static_assert(!M::ncf && (M::K == 16 || M::K == 32 || M::K == 64), "MF k in {16, 32, 64}");
   constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, TPC = kChunk / 16;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -3382,9 +2874,11 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
                      "+v"(bd[6]), "+v"(bd[7]), "+v"(bd[8]), "+v"(bd[9]), "+v"(bd[10]), "+v"(bd[11]),
                      "+v"(bd[12]), "+v"(bd[13]), "+v"(bd[14]), "+v"(bd[15]));
-      else
+      else if constexpr (KS == 8)
         asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
                      "+v"(bd[6]), "+v"(bd[7]));
+      else
+        asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]));
       d4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int sl = 0; sl < KS; ++sl) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sl], bd[sl], acc, 0, 0, 0);
@@ -3883,9 +3377,9 @@ static int solve_mode() {
   return m;
 }
 
-// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): old (default) | run
+// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): runs (default) | old
 static const char* mf_score_mode() {
-  static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "old";
+  static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "runs";
   return m;
 }
 
@@ -3953,27 +3447,9 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
       FIA_HIP_TRY(hipGetLastError());
     }
   } else {
-    // e_p per list position of each side, for the scoring kernels
-    FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * X.N + 1), s));
-    for (int sd = 0; sd < 2; ++sd) {
-      G.emb_self[sd] = c->p.t[sd];
-      G.bias_self[sd] = c->p.t[2 + sd];
-      G.bias_other[sd] = c->p.t[3 - sd];
-      G.rating[sd] = X.side[sd].rating.as<float>();
-    }
-    G.gbias = c->p.t[4];
-    // per-list-position residuals (fused into the Gram pass): read by k_score_mf_run only
-    G.lres = (M::K <= 16 && !strcmp(mf_score_mode(), "run")) ? c->resid.as<double>() : nullptr;
     if (G.n_items[0] + G.n_items[1] > 0) {
       hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
       FIA_HIP_TRY(hipGetLastError());
-      // the residual pass as its own launch over the same work items (fused into the Gram
-      // wave it raised that kernel's VGPRs 64 -> 128: ml-1m-ex prepare 78 -> 88 us)
-      if (G.lres) {
-        hipLaunchKernelGGL(k_resid_list_mf<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
-      }
-      FIA_HIP_TRY(hipGetLastError());
-
     }
   }
   const int64_t nc0 = n_ent[0] > 0 ? X.n_gcomb[0] : 0, nc1 = n_ent[1] > 0 ? X.n_gcomb[1] : 0;
@@ -3997,7 +3473,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // (ml-1m-ex 36.6 vs 39.3 M q/s).  NCF scoring is entity-shared only (k_score_ncf).
   const bool grouped = M::ncf || (c->score_mode >= 0 ? c->score_mode == 1 : M::K >= 32);
   // MF k in {32, 64} at K <= 1: the f64-MFMA entity-shared kernel (query blocks of 15)
-  constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);
+  constexpr bool mfma_ok = !M::ncf && (M::K == 16 || M::K == 32 || M::K == 64);
   static const bool mfma_on = !getenv("FIA_NO_MFMA_SCORE");   // A/B knob: k_score_grouped_mf instead
   const bool use_mfma = mfma_ok && grouped && K <= 1 && mfma_on;
   // A/B knobs of the MFMA kernel's variants (FIA_MFMA_CPI=1: one chunk per work item;
@@ -4011,7 +3487,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // MF k <= 16 per-query chunks: k_score_mf (default) or k_score_mf_run (A/B knob
   // FIA_MF_SCORE=run), one candidate slot set per chunk
   const char* mfs = mf_score_mode();
-  const bool runs = !M::ncf && M::K <= 16 && !grouped && !strcmp(mfs, "run");
+  const bool runs = !M::ncf && M::K <= 16 && !grouped && strcmp(mfs, "old") != 0;
   const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   if (K > 0) {
@@ -4026,7 +3502,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // solve and finished full-D; the chunk scan zeroes the count
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
-  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs));
+  // MF k <= 16 item runs: one wave per equal-cost slice of the descriptor list (descriptor
+  // costs vary ~10x: a static stride over descriptors left waves idle for half the kernel);
+  // the slice count is known on the device only -- the grid is its bound (total cost <=
+  // kRunUserCost per descriptor slot), the surplus waves exit at once
+  static const int64_t genv = getenv("FIA_SCORE_GRID") ? atoll(getenv("FIA_SCORE_GRID")) : 0;  // A/B knob
+  static const int lam_env = getenv("FIA_RUNS_LAMBDA") ? atoi(getenv("FIA_RUNS_LAMBDA")) : 0;  // A/B knob
+  const int64_t lam = lam_env > 0 ? lam_env : 32;
+  const int64_t runs_grid = (kRunUserCost * (max_chunks + 1)) / lam + 2;
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? cpi_used : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
@@ -4099,9 +3583,9 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   int64_t grid = (max_items + 3) / 4;            // 4 waves (work items) per block
   if (grid < 1) grid = 1;
   // grid cap (measured): NCF 1024 workgroups (yelp-ex score 0.314 -> 0.290 ms), MF 8192
-  static const int64_t genv = getenv("FIA_SCORE_GRID") ? atoll(getenv("FIA_SCORE_GRID")) : 0;  // A/B knob
   const int64_t gcap = genv > 0 ? genv : M::ncf ? 1024 : 8192;
   if (grid > gcap) grid = gcap;
+  if (runs) grid = runs_grid;
   phase_begin(c, 2, s);
   if (grouped) {
     if constexpr (M::ncf)
@@ -4134,15 +3618,13 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
                          c->cand_val.as<double>());
   } else {
-    // A/B knob FIA_MF_SCORE: old (default, k_score_mf) | run (opt-in item runs, k_score_mf_run)
+    // MF k <= 16: item runs (k_score_mf_runs); FIA_MF_SCORE=old: the per-query chunk kernel
     if constexpr (!M::ncf) {
       if constexpr (M::K <= 16) {
         if (runs) {
-          hipLaunchKernelGGL(k_score_mf_run<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, Q,
-                             c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
-                             c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
-                             c->cand_val.as<double>());
-          FIA_HIP_TRY(hipGetLastError());
+          FIA_HIP_TRY(launch_score_mf_runs(M::K, grid, s, A, Q, c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
+                                           c->slices.as<int32_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                                           c->cand_pos.as<int32_t>(), c->cand_val.as<double>()));
           phase_end(c, 2, s);
           goto topk;
         }
@@ -4287,13 +3769,9 @@ hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* 
                          topk_val, s, x_in);
   FIA_MODEL_CASES(X)
 #undef X
-  if (x_in) {                          // large k: scoring from a given x is not built
-    unsupported = true;
-    return hipSuccess;
-  }
   if (big_supported(c->p.model, c->p.k))
     return query_big(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos, topk_idx, topk_val,
-                     s);
+                     s, x_in);
   unsupported = true;
   return hipSuccess;
 }

@@ -176,6 +176,11 @@ class Context(object):
         self._need_int32(rel_idx, "rel_idx")
         if x_in.dtype != torch.float64 or not x_in.is_contiguous():
             raise TypeError("x_in must be a contiguous torch.float64 tensor")
+        if not x_in.is_cuda:
+            raise TypeError("x_in must be a device (cuda) tensor")
+        if x_in.numel() < qu.numel() * self.num_params():
+            raise ValueError("x_in holds %d values, %d queries need %d" % (
+                x_in.numel(), qu.numel(), qu.numel() * self.num_params()))
         rc = self.lib.fia_query_batch_x(self.h, qu.numel(), _ptr(qu), _ptr(qi), _ptr(offsets), int(total),
                                         _ptr(x_in), _ptr(rel_idx), _ptr(influence), int(K), _ptr(topk_pos),
                                         _ptr(topk_idx), _ptr(topk_val), _stream())

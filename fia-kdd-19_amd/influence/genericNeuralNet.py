@@ -422,12 +422,22 @@ class GenericNeuralNet(object):
             self.model_name, approx_type, loss_type, test_description))
         # the reference's cached inverse HVP (mf:210-214): with force_refresh False and the
         # file present, its vector replaces the solve (scored on the GPU, fia_query_batch_x)
+        # Only a flat float64 vector of this model's D values is accepted: the reference
+        # itself saves a ragged per-block list (mf:221), which numpy stores as an object
+        # array that allow_pickle=False refuses -- such a file, or one of another size, is
+        # treated as absent and the solve runs (pickles are never loaded).
         cached = None
         if not force_refresh and os.path.exists(fname):
-            with np.load(fname, allow_pickle=False) as z:
-                cached = np.asarray(z["inverse_hvp"], np.float64).reshape(1, -1)
+            try:
+                with np.load(fname, allow_pickle=False) as z:
+                    arr = np.asarray(z["inverse_hvp"])
+                if arr.dtype.kind == "f" and arr.size == self.ctx.num_params():
+                    cached = arr.astype(np.float64).reshape(1, -1)
+            except (ValueError, KeyError, OSError):
+                cached = None
             if self.verbose:
-                print("Loaded inverse HVP from %s" % fname)
+                print(("Loaded inverse HVP from %s" if cached is not None else
+                       "Ignored unusable inverse HVP file %s") % fname)
         # (the caller's own profiling mask and unread sums are kept: Context.profiled_call)
         res, phases = self.ctx.profiled_call(
             lambda: self.get_influence_batch(test_indices, K=0, full=True, return_x=True, inverse_hvp=cached))

@@ -140,8 +140,9 @@ int fia_query_batch(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, co
  * the reference theta order, as fia_query_batch's x_out) replaces H_t^-1 v; the related sets,
  * influence and top-K follow from it exactly as in fia_query_batch.  Replaces the reference's
  * cached-inverse-HVP branch of get_influence_on_test_loss (force_refresh=False and an existing
- * <model>-cg-normal_loss-test-[t].npz, matrix_factorization.py:210-214).  Small-k models only
- * (MF k <= 64, NCF k <= 32); large k returns FIA_ERR_UNSUPPORTED. */
+ * <model>-cg-normal_loss-test-[t].npz, matrix_factorization.py:210-214).  Every built model:
+ * small k records from x directly (k_record_x); large k (MF k >= 128, NCF k >= 64) skips the
+ * batched LDL^T panels and writes the padded solution and records from x (k_big_record_x). */
 int fia_query_batch_x(fia_ctx* ctx, int64_t num_queries, const int32_t* q_user, const int32_t* q_item,
                       const int64_t* offsets, int64_t total_rel, const double* x_in,
                       int32_t* rel_idx, double* influence,

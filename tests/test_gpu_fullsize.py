@@ -165,12 +165,21 @@ def test_config4_mf64_all_queries(data20m):
     order = np.lexsort((qu, qi))                       # bench.py's item-major batching
     qu, qi = np.ascontiguousarray(qu[order]), np.ascontiguousarray(qi[order])
     deg_i = np.bincount(d["train"][1], minlength=d["I"])
+    deg_u = np.bincount(d["train"][0], minlength=d["U"])
     heavy = int(np.argmax(deg_i[qi]))
+    # >= 200 oracle queries spread over every batch: 9 per batch of the bench's batching
+    cum = np.concatenate([[0], np.cumsum(deg_u[qu] + deg_i[qi])])
+    starts = [0]
+    while starts[-1] < qu.size:
+        b0 = starts[-1]
+        starts.append(min(qu.size, max(int(np.searchsorted(cum, cum[b0] + BATCH_ROWS, side="right")) - 1, b0 + 1)))
     rng = np.random.default_rng(0)
-    keep = [heavy] + [int(q) for q in rng.choice(qu.size, 4, replace=False)]
+    keep = [heavy] + [int(q) for b0, b1 in zip(starts[:-1], starts[1:])
+                      for q in rng.choice(np.arange(b0, b1), min(9, b1 - b0), replace=False)]
     checker = GpuChecker(d)
     got, nb, n_q = run_batches(ctx, qu, qi, 1, checker, keep)
     assert qu.size == 276986 and nb > 1 and n_q.sum() > 1e10
+    assert nb == len(starts) - 1 and len(set(keep)) >= 200, (nb, len(set(keep)))
     oracle = fo.CsrExact("MF", params, 64, *d["train"], 1e-3, 1e-6)
     for q in keep:
         compare_oracle("MF", 64, d, params, int(qu[q]), int(qi[q]), got[q], oracle)
@@ -237,10 +246,12 @@ def test_config3_yelp_ncf_all_queries():
     deg_i = np.bincount(d["train"][1], minlength=d["I"])
     heavy = int(np.argmax(deg_i[qi]))
     rng = np.random.default_rng(2)
-    keep = [heavy] + [int(q) for q in rng.choice(qu.size, 11, replace=False)]
+    keep = [heavy] + [int(q) for q in rng.choice(qu.size, 2000, replace=False)]
     got, nb, n_q = run_batches(ctx, qu, qi, 1, GpuChecker(d), keep)
-    assert nb == 1
+    assert nb == 1 and len(set(keep)) >= 2000
+    from oracle import fia_oracle as fo
+    oracle = fo.CsrExact("NCF", params, 16, *d["train"], 1e-3, 1e-6)
     for q in keep:
-        compare_oracle("NCF", 16, d, params, int(qu[q]), int(qi[q]), got[q])
+        compare_oracle("NCF", 16, d, params, int(qu[q]), int(qi[q]), got[q], oracle)
     ctx.close()
     torch.cuda.empty_cache()
