@@ -11,22 +11,25 @@ resident in HBM.
 Multi-GPU (one process per GPU).  `--gpus N` without a launcher
 re-launches this script under torch.distributed.run with N ranks before anything
 touches the GPU; under torchrun (the driver) WORLD_SIZE/RANK/LOCAL_RANK are read
-from the environment.  Scaling (`--scaling`, default per config):
-  * strong (20M configs): the fixed query set (276,986 held-out pairs) is split into
-    N contiguous ranges balanced by the related-set sizes n_q (influence.sharding.
-    shard_ranges); every rank answers its range;
-  * weak (ml-1m-ex, yelp-ex): every rank answers one full-size query set -- rank 0
-    the workload's own pairs, rank r > 0 the same users and item multiset re-paired
-    by a seeded permutation (distinct pairs, none a training row).
+from the environment.  Scaling (`--scaling`; every config defaults to strong):
+  * strong: the config's fixed query set is split into N contiguous ranges balanced
+    by the related-set sizes n_q (influence.sharding.shard_ranges); every rank
+    answers its range.  On one GPU, `--shard-of S --shard-index r` answers range r
+    of an S-way split (one rank's share of an S-GPU job);
+  * weak (opt-in): every rank answers one full-size query set -- rank 0 the
+    workload's own pairs, rank r > 0 the same users and item multiset re-paired by
+    a seeded permutation (distinct pairs, none a training row).
 The only exchange is the RCCL all_gather of the per-query top-K lists, overlapped
 with the next step.  `value` = queries answered by all ranks / the max-over-ranks
 time of the timed steps.
 
-Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (the scoring
-kernel): `achieved` = its HBM bytes per launch measured by rocprofv3 PMC
-(FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction; profiles/
-score_traffic.json) over its HIP-event duration in this run, `frac` = achieved /
-8 TB/s; SURVEY 8d's algorithmic byte count sits beside it under `algorithmic`.
+Rank 0 prints one JSON line.  `roofline` prices the step's dominant phase (from a few
+instrumented steps): the scoring phase against HBM -- `achieved` = its kernel's HBM
+bytes per launch measured by rocprofv3 PMC (FETCH_SIZE x 2 + WRITE_SIZE,
+MI355X_MICROARCH.md's gfx950 correction; profiles/traffic.json, tools/traffic_json.py)
+over its HIP-event duration in this run, `frac` = achieved / 8 TB/s, with SURVEY 8d's
+algorithmic byte count beside it under `algorithmic` -- or a solve / prepare phase
+against the FP64 peak (algorithmic flops over its event time).
 `cpu_baseline` times the reference ALGORITHM (oracle/ncg_port.py) on a bounded
 sample on this host, with two more CPU figures under `variants`.
 """
@@ -76,8 +79,10 @@ def parse(argv=None):
     ap.add_argument("--batch-rows", type=int, default=1 << 29,
                     help="max related ratings per fia_query_batch call (output buffers are reused)")
     ap.add_argument("--shard-of", type=int, default=1,
-                    help="answer only shard 0 of S of the strong-scaling split (with S=8 at N=1: one GPU's share "
+                    help="answer only one shard of S of the strong-scaling split (with S=8 at N=1: one GPU's share "
                          "of the 8-GPU job)")
+    ap.add_argument("--shard-index", type=int, default=0,
+                    help="with --shard-of S at N=1: which shard (0 .. S-1) to answer")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
     ap.add_argument("--spinup-seconds", type=float, default=None,
@@ -134,14 +139,11 @@ def solve_kernel(cfg):
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_bs_trail"              # batched blocked LDL^T panels (+ k_bs_dupd/dfac/back)
-    mode = os.environ.get("FIA_SOLVE", "")
-    if mode == "cols":
-        return "k_solve"
     if model == "MF" and k <= 16:
         return "k_solve_tps"
-    if model == "NCF" and k == 16 and mode not in ("tile", "col"):
+    if model == "NCF" and k == 16:
         return "k_solve_rows"            # (+ k_ncf_query_pro, the thread-per-query MLP prologue)
-    if model == "NCF" and k <= 16 and mode != "tile":
+    if model == "NCF" and k == 8:
         return "k_solve_col"
     return "k_solve_tile"
 
@@ -175,16 +177,15 @@ def prepare_flops(model, k, N):
 
 def score_kernel(cfg, K=1):
     """The library's scoring kernel for this config (the dispatch in models.hip query_impl /
-    bigk.hip query_big_impl, including their environment switches)."""
+    bigk.hip query_big_impl: one kernel per (model, k, top-K))."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
-        return "k_big_score" if os.environ.get("FIA_BIG_SCORE_VALU") else "k_big_score_mfma"
+        return "k_big_score_mfma"
     if model == "NCF":
         return "k_score_ncf"
     if k <= 16:
-        mode = os.environ.get("FIA_MF_SCORE", "old")
-        return "k_score_mf_run" if mode == "run" else "k_score_mf"
-    if k in (32, 64) and K <= 1 and not os.environ.get("FIA_NO_MFMA_SCORE"):
+        return "k_score_mf_runs"
+    if K <= 1:
         return "k_score_mf_mfma"
     return "k_score_grouped_mf"
 
@@ -456,7 +457,11 @@ def main():
         S = world if world > 1 else args.shard_of
         rs = shard_ranges(n_q, S)
         all_sizes = [b - a for a, b in rs][:world] if world > 1 else [rs[0][1] - rs[0][0]]
-        b0, b1 = rs[rank if world > 1 else 0]
+        if world == 1 and not 0 <= args.shard_index < S:
+            raise SystemExit("bench: --shard-index %d outside 0 .. %d" % (args.shard_index, S - 1))
+        b0, b1 = rs[rank if world > 1 else args.shard_index]
+        if world == 1:
+            all_sizes = [b1 - b0]
         qu_np, qi_np, n_q = qu_np[b0:b1], qi_np[b0:b1], n_q[b0:b1]
         qu, qi = qu[b0:b1].contiguous(), qi[b0:b1].contiguous()
         shard_of = S
@@ -655,7 +660,9 @@ def main():
                    "model": cfg["model"], "k": k, "queries_per_rank": all_sizes,
                    "node_queries_per_step": node_queries, "n_train": int(tu.size),
                    "related_ratings_rank0_step": int(total), "topk": K, "query_batches": len(batches),
-                   "query_order": args.query_order, "shard_of": shard_of, "hip_graph": use_graph,
+                   "query_order": args.query_order, "shard_of": shard_of,
+                   "shard_index": (rank if world > 1 else args.shard_index) if shard_of > 1 else None,
+                   "hip_graph": use_graph,
                    "spinup_steps": n_spin,
                    "dist_backend": backend if world > 1 else None,
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},

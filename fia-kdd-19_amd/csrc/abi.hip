@@ -104,10 +104,6 @@ int fia_create(int device, fia_ctx** out) {
   fia_ctx* c = new (std::nothrow) fia_ctx();
   if (!c) return FIA_ERR_NOMEM;
   c->device = device;
-  // scoring schedule override (A/B knob for profiling): FIA_SCORE=chunk (per-query chunks)
-  // or grouped (entity chunks shared by the batch's queries of that entity); default: the
-  // model decides (query_model)
-  if (const char* m = getenv("FIA_SCORE")) c->score_mode = std::string(m) == "grouped" ? 1 : 0;
   *out = c;
   return FIA_OK;
 }

@@ -21,8 +21,8 @@
 //     along as the matrix's extra last row, so its row of L is D^-1 L^-1 v and only the
 //     backward solve L^T x = y remains;
 //   * scoring over entity chunks shared by every query of the batch with that entity
-//     (k_big_score): the gathered rows / d1_j / e_j are loaded once per chunk and
-//     dotted with up to 8 query vectors.
+//     (k_big_score_mfma): the gathered rows / d1_j / e_j are streamed once per chunk
+//     into 16 x 16 f64 MFMA products against blocks of 16 query vectors.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -1304,155 +1304,13 @@ __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __re
 }
 
 // ------------------------------------------------------------------------------------
-// Entity-shared scoring (work items from build_groups: one <= kChunk chunk of one
-// entity's list x one block of <= kBigQueryBlock queries with that entity).  Per rating:
+// Entity-shared scoring on the f64 matrix cores (work items from build_groups: one
+// <= kChunk chunk of one entity's list x one block of <= kBigMfmaQB queries with that
+// entity).  Per rating:
 //   MF  s_q = x_emb,q . emb_other + x_bias,q
 //   NCF s_q = x_mlp,q . g_mlp,j + (W3g * x_gmf,q) . gmf_other
 //   influence = (2 e_j s_q + c_q) / n_q   (mf:240-246); the test pair's own train row
-//   takes e and s = x.v from the record (bit-identical copies).
-// ------------------------------------------------------------------------------------
-template <class M>
-constexpr int score_waves() {
-  return (4 + M::SB) * kBigQueryBlock * 8 > 20000 ? 2 : 4;
-}
-
-template <class M>
-__global__ __launch_bounds__(64 * score_waves<M>()) void k_big_score(
-    BigArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
-    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
-    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  constexpr int K = M::K, SW = score_waves<M>(), QB = kBigQueryBlock, RSW = 4 + M::SB;
-  constexpr int NPASS = kScoreRows;
-  __shared__ double srec[SW][QB * RSW];
-  __shared__ int64_t sbase[SW][3 * QB];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n_items = wstart[nE];
-  const int64_t stride = (int64_t)gridDim.x * SW;
-  for (int64_t wi = (int64_t)blockIdx.x * SW + wave; wi < n_items; wi += stride) {
-    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
-    const int sd = g >= A.U ? 1 : 0;
-    const int32_t e = sd ? (int32_t)(g - A.U) : g;
-    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
-    const int64_t rem = A.ptr[sd][e + 1] - lb;
-    const int len = rem < kChunk ? (int)rem : kChunk;
-    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
-    const int64_t gn = gstart[g + 1] - gb;
-    const int nq = gn < QB ? (int)gn : QB;
-    const int32_t* __restrict__ oth = A.other[sd] + lb;
-    const float* __restrict__ rat = A.rating[sd] + lb;
-    const int32_t* __restrict__ rw = A.row[sd] + lb;
-    const float* __restrict__ T = M::ncf ? (sd == 0 ? A.t[3] : A.t[2]) : (sd == 0 ? A.t[1] : A.t[0]);
-    double* __restrict__ rl = srec[wave];
-    int64_t* __restrict__ bl = sbase[wave];
-    __builtin_amdgcn_wave_barrier();
-    for (int t = lane; t < QB * RSW; t += 64) {
-      const int j = t / RSW, c = t - j * RSW;
-      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
-      rl[t] = rec[(int64_t)q * M::R + (c < 4 ? c : 8 + sd * M::SB + (c - 4))];
-    }
-    if (lane < QB) {
-      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
-      const int64_t* qb = qbase + 4 * (int64_t)q;
-      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
-      bl[QB + lane] = qb[2 + sd] + cidx;
-      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-    for (int h = 0; h < NPASS; ++h) {
-      const int idx = h * 64 + lane;
-      const bool ok = idx < len;
-      const int li = ok ? idx : 0;
-      const int32_t o = oth[li], row = rw[li];
-      const float y = rat[li];
-      const double ej = A.resid[row];
-      double s[QB];
-#pragma unroll
-      for (int j = 0; j < QB; ++j) s[j] = 0.0;
-      const float4* __restrict__ src = reinterpret_cast<const float4*>(T + (int64_t)o * K);
-      constexpr int OFF_B = M::ncf ? K : 0;   // record offset of the vector dotted with the gathered row
-#pragma unroll 2
-      for (int c4 = 0; c4 < K / 4; c4 += 2) {
-        const float4 v0 = src[c4], v1 = src[c4 + 1];
-        const double g8[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int j = 0; j < QB; ++j) {
-          if (j >= nq) break;
-          const double* xr = rl + j * RSW + 4 + OFF_B + 4 * c4;
-#pragma unroll
-          for (int cc = 0; cc < 8; ++cc) s[j] = fma(xr[cc], g8[cc], s[j]);
-        }
-      }
-      if constexpr (M::ncf) {
-        const double2* __restrict__ dsrc = reinterpret_cast<const double2*>(A.gm[sd] + (int64_t)row * K);
-#pragma unroll 2
-        for (int c2 = 0; c2 < K / 2; c2 += 2) {
-          const double2 a0 = dsrc[c2], a1 = dsrc[c2 + 1];
-          const double g4[4] = {a0.x, a0.y, a1.x, a1.y};
-#pragma unroll
-          for (int j = 0; j < QB; ++j) {
-            if (j >= nq) break;
-            const double* yr = rl + j * RSW + 4 + 2 * c2;
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) s[j] = fma(yr[cc], g4[cc], s[j]);
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < QB; ++j) {
-        if (j >= nq) break;
-        const double* __restrict__ Rj = rl + j * RSW;
-        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat = Rj[3];
-        double ss = s[j], ee = ej;
-        double dup;
-        if constexpr (!M::ncf) {
-          ss += Rj[4 + K];
-          dup = Rj[4 + K + 1];
-        } else {
-          dup = Rj[4 + 2 * K];
-        }
-        if ((double)o == dup) { ee = rhat - (double)y; ss = xv; }
-        const double infl = (2.0 * ee * ss + cq) * inv_n;
-        const int64_t obj = bl[j];
-        if (ok) {
-          if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-          if (rel_idx) __builtin_nontemporal_store(row, rel_idx + obj + idx);
-        }
-        if (K_top > 0) {
-          const int64_t cbj = bl[QB + j];
-          const int64_t poj = bl[2 * QB + j];
-          const double la = ok ? topk_key(infl) : -2.0;
-          const int lp = ok ? cidx * kChunk + idx : -1;
-          double pa = INFINITY;
-          int pp = -1;
-          for (int t = 0; t < K_top; ++t) {
-            double ba = -2.0, bv = 0.0;
-            int bp = 0x7fffffff;
-            if (lp >= 0 && better(pa, pp, la, lp)) { ba = la; bp = lp; bv = infl; }
-            wave_best(ba, bp, bv);
-            if (lane == 0) {
-              const bool okk = ba > -1.5;
-              const int64_t slot = (cbj * NPASS + h) * K_top + t;
-              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
-              cand_val[slot] = okk ? bv : NAN;
-            }
-            pa = ba;
-            pp = bp;
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Entity-shared scoring on the f64 matrix cores (same work items, same outputs and
-// top-K candidate slots as k_big_score, blocks of kBigMfmaQB queries).  A workgroup
+//   takes e and s = x.v from the record (bit-identical copies).  A workgroup
 // takes one work item; wave h is scoring pass h (ratings [64 h, 64 h + 64) of the
 // chunk, four 16-rating tiles).  Per tile the scores are one 16 x 16 MFMA product
 // over the dotted length KD (MF: x_emb . emb_other; NCF: x_mlp . g_mlp,j then
@@ -1860,8 +1718,7 @@ hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, c
   constexpr int kLast = NP % kBsNB == 0 ? kBsNB : NP % kBsNB;   // last panel's width
   if (max_sys <= 0) return hipSuccess;
   constexpr int64_t slab = bs_slab<NP>();
-  static const int64_t scratch = getenv("FIA_BS_SCRATCH_MB") ? atoll(getenv("FIA_BS_SCRATCH_MB")) << 20 : kBsScratch;
-  int64_t S = scratch / (int64_t)(sizeof(double) * slab);
+  int64_t S = kBsScratch / (int64_t)(sizeof(double) * slab);
   S = S < 1 ? 1 : (S > max_sys ? max_sys : S);
   FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(S * slab), s));
   for (int64_t w0 = 0; w0 < max_sys; w0 += S) {
@@ -1884,7 +1741,7 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
                           int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                           int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
                           const double* x_in) {
-  constexpr int NPs = M::NPs, NPASS = kScoreRows, SW = score_waves<M>();
+  constexpr int NPs = M::NPs, NPASS = kScoreRows;
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * M::QW + 1), s));
   FIA_HIP_TRY(c->xb.reserve(sizeof(double) * (size_t)(Q * 2 * NPs + 1), s));
@@ -1897,8 +1754,7 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   const BigArgs A = make_big_args(c, qu, qi);
   phase_begin(c, 4, s);
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, true, s));
-  const bool mfma_score = !getenv("FIA_BIG_SCORE_VALU");
-  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, mfma_score ? kBigMfmaQB : kBigQueryBlock, s));
+  FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_chunks, kBigMfmaQB, s));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   FIA_HIP_TRY(hipMemsetAsync(c->syslist.ptr, 0, sizeof(int32_t), s));
@@ -1913,10 +1769,7 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
                          (const double*)c->qwork.as<double>(), c->xb.as<double>(), c->rec.as<double>());
     FIA_HIP_TRY(hipGetLastError());
   } else {
-    if (!getenv("FIA_BIG_SOLVE_PERSISTENT"))
-      FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
-    else
-      FIA_HIP_TRY((launch_solve<M, NPs, false>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
+    FIA_HIP_TRY((launch_solve_batched<M, NPs>(c, A, 2 * Q, c->syslist.as<int32_t>(), s)));
     FIA_HIP_TRY((launch_solve<M, 2 * NPs, true>(c, A, Q, c->cpllist.as<int32_t>(), s)));
   }
   hipLaunchKernelGGL(k_big_finish<M>, dim3(grid_cap(Q, 1 << 20)), dim3(64), 0, s, Q, c->qwork.as<double>(),
@@ -1924,16 +1777,10 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
   phase_begin(c, 2, s);
-  if (mfma_score)
-    hipLaunchKernelGGL(k_big_score_mfma<M>, dim3(grid_cap(max_chunks, 8192)), dim3(256), 0, s, A, c->p.U + c->p.I,
-                       c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
-                       c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
-                       c->cand_val.as<double>());
-  else
-    hipLaunchKernelGGL(k_big_score<M>, dim3(grid_cap((max_chunks + SW - 1) / SW, 8192)), dim3(64 * SW), 0, s, A,
-                       c->p.U + c->p.I, c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
-                       c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+  hipLaunchKernelGGL(k_big_score_mfma<M>, dim3(grid_cap(max_chunks, 8192)), dim3(256), 0, s, A, c->p.U + c->p.I,
+                     c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
+                     c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
+                     c->cand_val.as<double>());
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);
   if (K > 0) {

@@ -34,7 +34,6 @@ constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
-constexpr int kBigQueryBlock = 8;        // ... large k (register-resident per-query sums)
 
 // Device buffer with grow-on-demand capacity (never shrinks), allocated from the
 // device's stream-ordered pool on the context's stream: growing a buffer frees the old
@@ -228,7 +227,6 @@ struct fia_ctx {
   // on the calling stream only)
   hipStream_t stream = nullptr;
   bool has_stream = false;
-  int score_mode = -1;    // scoring schedule: -1 auto, 0 per-query chunks, 1 entity-shared (FIA_SCORE)
   unsigned profiling = 0;   // bit p: record phase p (fia_set_profiling)
   fia::PhaseEvents events;
 };
@@ -251,7 +249,6 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr,
                         bool runs = false, int slice_cost = 0);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
-int64_t gram_chunk(int64_t want);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_items, int qb, hipStream_t s, int cpi = 1);

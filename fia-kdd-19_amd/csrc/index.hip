@@ -144,6 +144,13 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   __shared__ int s_tile;
   __shared__ int64_t s_wave[kScanThreads / 64], s_wave2[kScanThreads / 64];
   __shared__ int64_t s_prefix, s_prefix2;
+  // runs mode: per-query fill state (descriptor start, -1 = no descriptors; cost prefix;
+  // list bases and lengths; output base; run length; descriptor count)
+  __shared__ int64_t f_c0[MODE == 1 ? kScanTile : 1], f_cost[MODE == 1 ? kScanTile : 1];
+  __shared__ int64_t f_ub[MODE == 1 ? kScanTile : 1], f_ib[MODE == 1 ? kScanTile : 1];
+  __shared__ int64_t f_base[MODE == 1 ? kScanTile : 1];
+  __shared__ int32_t f_du[MODE == 1 ? kScanTile : 1], f_di[MODE == 1 ? kScanTile : 1];
+  __shared__ int32_t f_nq[MODE == 1 ? kScanTile : 1], f_nd[MODE == 1 ? kScanTile : 1];
   const unsigned ntiles = (unsigned)((Q + 1 + kScanTile - 1) / kScanTile);
   if (threadIdx.x == 0) s_tile = (int)atomicAdd(&tctr[0], 1u);
   __syncthreads();
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
         s_ub[it] = ub; s_du[it] = du; s_ib[it] = ib; s_di[it] = di;
         x = MODE == 0 ? du + di : (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
         if (MODE == 1 && runs) {
-          // packed {chunks (candidate slots) << 31 | work descriptors}, chunks of clen ratings:
+          // packed {chunks (candidate slots) << 31 | work descriptors}, chunks of kRunChunk ratings:
           // the item-side chunks are work only for a run head (first query of a run of equal
           // test items, runs cut at multiples of `runs`), which scores them for the whole run
           const bool head = (q % runs) == 0 || qi[q - 1] != i;
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
             }
             s_nq[it] = nq;
           }
-          const int64_t cu = (du + clen - 1) / clen, ci = (di + clen - 1) / clen;
+          const int64_t cu = (du + kRunChunk - 1) / kRunChunk, ci = (di + kRunChunk - 1) / kRunChunk;
           x = ((cu + ci) << 31) | (cu + (head ? ci : 0));
           tsum2 += cu * kRunUserCost + (head ? ci * (s_nq[it] + 2) : 0);
         }
@@ -251,45 +258,19 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
       qbase[4 * q + 0] = s_base[it];
       qbase[4 * q + 1] = s_base[it] + du;
       qbase[4 * q + 2] = cr;
-      qbase[4 * q + 3] = cr + (du + (runs ? clen : kChunk) - 1) / (runs ? clen : kChunk);
+      qbase[4 * q + 3] = cr + (runs ? (du + kRunChunk - 1) / kRunChunk : (du + kChunk - 1) / kChunk);
     }
-    if (MODE == 1 && runs && cdesc && q < Q && v[it] > 0) {
-      const int64_t ub = s_ub[it], du = s_du[it], ib = s_ib[it], di = s_di[it];
-      int64_t c = run & kLo;
-      const int64_t base = s_base[it];
-      // descriptor c with cost w at cost prefix p starts every slice whose start point
-      // s * lam lies in [p, p + w) (slices of a descriptor costing more than lam but the
-      // last are empty): every descriptor lands in exactly one slice
-      // (lam = 1 << lsh: shifts, no 64-bit division in this per-descriptor loop)
-      int64_t p = run2;
-      auto mark = [&](int64_t cd, int64_t w) {
-        if (slices)
-          for (int64_t sl = (p + (1ll << lsh) - 1) >> lsh; (sl << lsh) < p + w; ++sl) slices[sl] = (int32_t)cd;
-        p += w;
-      };
-      for (int64_t st = 0; st < du; st += clen, ++c) {
-        ChunkDesc d;
-        d.list_base = ub + st;
-        d.out_base = base + st;
-        d.q = (int32_t)q;
-        d.pos0 = (int32_t)st;
-        d.len = (int32_t)(du - st < clen ? du - st : clen);
-        d.side = 0 | (1 << 8);
-        cdesc[c] = d;
-        mark(c, kRunUserCost);
-      }
-      if (s_nq[it] > 0)
-        for (int64_t st = 0; st < di; st += clen, ++c) {
-          ChunkDesc d;
-          d.list_base = ib + st;
-          d.out_base = base + du + st;
-          d.q = (int32_t)q;
-          d.pos0 = (int32_t)(du + st);
-          d.len = (int32_t)(di - st < clen ? di - st : clen);
-          d.side = 1 | (s_nq[it] << 8);
-          cdesc[c] = d;
-          mark(c, s_nq[it] + 2);
-        }
+    if (MODE == 1 && runs) {
+      // runs mode: this query's descriptors are written by the whole block below
+      f_c0[threadIdx.x] = run & kLo;
+      f_cost[threadIdx.x] = run2;
+      f_ub[threadIdx.x] = s_ub[it];
+      f_ib[threadIdx.x] = s_ib[it];
+      f_base[threadIdx.x] = s_base[it];
+      f_du[threadIdx.x] = (int32_t)s_du[it];
+      f_di[threadIdx.x] = (int32_t)s_di[it];
+      f_nq[threadIdx.x] = s_nq[it];
+      f_nd[threadIdx.x] = (q < Q) ? (int32_t)(v[it] & kLo) : 0;
     } else
     if (MODE == 1 && cdesc && q < Q && v[it] > 0) {
       const int64_t ub = s_ub[it], du = s_du[it], ib = s_ib[it], di = s_di[it];
@@ -317,9 +298,58 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
       }
     }
     run += v[it];
-    if (MODE == 1 && runs && q < Q && v[it] > 0) {
-      const int64_t cu = (s_du[it] + clen - 1) / clen, ci = (s_di[it] + clen - 1) / clen;
-      run2 += cu * kRunUserCost + (s_nq[it] > 0 ? ci * (s_nq[it] + 2) : 0);
+  }
+  if (MODE == 1 && runs && cdesc) {
+    // Block-parallel descriptor fill (runs mode): the block's descriptors are one contiguous
+    // range; thread t writes descriptors t, t + 256, ... of it, finding the owning query by a
+    // binary search over the per-query starts in LDS (a popular item's run head has ~20
+    // descriptors: one thread writing them in turn bounded this kernel).  Descriptor j of a
+    // query: user chunk j < cu (cost kRunUserCost), else item chunk j - cu (cost nq + 2); the
+    // descriptor whose cost range [p, p + w) holds a slice start s << lsh starts slice s
+    // (slices of a descriptor costing more than a slice are empty but the last): every
+    // descriptor lands in exactly one slice.
+    __syncthreads();
+    const int64_t dstart = f_c0[0], dend = f_c0[kScanTile - 1] + f_nd[kScanTile - 1];
+    {
+      for (int64_t c = dstart + threadIdx.x; c < dend; c += kScanThreads) {
+        // the owner: the last thread whose start is <= c (starts ascend; a thread with no
+        // descriptors shares its start with the next one, so it is never the last such)
+        int lo = 0, hi = kScanTile - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (f_c0[mid] <= c) lo = mid; else hi = mid - 1;
+        }
+        const int t = lo;
+        const int64_t j = c - f_c0[t];
+        const int32_t du = f_du[t], di = f_di[t], nq = f_nq[t];
+        const int64_t cu = (du + kRunChunk - 1) / kRunChunk;
+        const int64_t qq = tile * kScanTile + t;
+        ChunkDesc d;
+        int64_t p, w;
+        if (j < cu) {
+          const int64_t st = j * kRunChunk;
+          d.list_base = f_ub[t] + st;
+          d.out_base = f_base[t] + st;
+          d.pos0 = (int32_t)st;
+          d.len = (int32_t)(du - st < kRunChunk ? du - st : kRunChunk);
+          d.side = 0 | (1 << 8);
+          p = f_cost[t] + j * kRunUserCost;
+          w = kRunUserCost;
+        } else {
+          const int64_t st = (j - cu) * kRunChunk;
+          d.list_base = f_ib[t] + st;
+          d.out_base = f_base[t] + du + st;
+          d.pos0 = (int32_t)(du + st);
+          d.len = (int32_t)(di - st < kRunChunk ? di - st : kRunChunk);
+          d.side = 1 | (nq << 8);
+          p = f_cost[t] + cu * kRunUserCost + (j - cu) * (nq + 2);
+          w = nq + 2;
+        }
+        d.q = (int32_t)qq;
+        cdesc[c] = d;
+        if (slices)
+          for (int64_t sl = (p + (1ll << lsh) - 1) >> lsh; (sl << lsh) < p + w; ++sl) slices[sl] = (int32_t)c;
+      }
     }
   }
   // the last tile to finish resets the tile words and the counters for the next launch
@@ -481,16 +511,6 @@ __global__ void k_write_related(const int32_t* __restrict__ qu, const int32_t* _
 
 }  // namespace
 
-// list rows per small-k Gram work item: `want` (the model's choice), FIA_GRAM_CHUNK
-// overrides for A/B runs
-int64_t gram_chunk(int64_t want) {
-  static const long long env = [] {
-    const char* e = getenv("FIA_GRAM_CHUNK");
-    return e ? atoll(e) : 0LL;
-  }();
-  return env >= 32 ? (int64_t)env : want;
-}
-
 namespace {
 
 inline unsigned bits_for(int64_t n) {
@@ -607,7 +627,7 @@ hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_
     FIA_HIP_TRY(hipStreamSynchronize(s));
     X.hord[sd] = ord;
   }
-  FIA_HIP_TRY(build_gram_lists(c, gram_chunk(kGramChunk), s));
+  FIA_HIP_TRY(build_gram_lists(c, kGramChunk, s));
   keys_sorted.release(s);
   tmp.release(s);
   // pair set, load factor <= 1/2

@@ -77,188 +77,6 @@ __device__ void ldlt_solve(double* H, double* v, double* d, double* w, int lo, i
   }
 }
 
-// Packed column-major lower storage: column c (rows c..N-1) starts at cs(c).
-template <int N>
-__device__ __forceinline__ int cs(int c) { return c * N - (c * (c - 1)) / 2; }
-
-// Two independent N x N systems (the user and the item block of one query; the path for
-// blocks too large for solve_blocks_regs), each a packed column-major lower block
-// H + b*PN with right-hand side v + b*N, solved in place by a right-looking LDL^T in which
-// every lane owns whole columns: step j, lane c > j does A[r][c] -= A[r][j] * (A[c][j] /
-// A[j][j]) down its own column (rows r >= c).  The blocks go in turn, lane c owning
-// columns c, c + 64.
-template <int N>
-__device__ void ldlt_cols(double* __restrict__ Hb, double* __restrict__ vb) {
-  constexpr int PN = N * (N + 1) / 2;
-  constexpr int CSTEP = kSolveThreads;
-  const int lane = threadIdx.x;
-#pragma unroll 1
-  for (int b = 0; b < 2; ++b) {
-    const int cl = lane;
-    double* H = Hb + b * PN;
-    double* v = vb + b * N;
-    for (int j = 0; j < N; ++j) {
-      __syncthreads();
-      const double* Hj = H + cs<N>(j) - j;     // Hj[r] = A[r][j]
-      const double dj = Hj[j];
-      for (int c = cl; c < N; c += CSTEP) {
-        if (c > j) {
-          const double f = Hj[c] / dj;
-          double* Hc = H + cs<N>(c) - c;       // Hc[r] = A[r][c]
-          for (int r = c; r < N; ++r) Hc[r] = fma(-Hj[r], f, Hc[r]);
-        }
-      }
-    }
-    __syncthreads();
-    for (int c = cl; c < N; c += CSTEP) {      // L[r][c] = A[r][c] / d_c
-      double* Hc = H + cs<N>(c) - c;
-      const double inv = 1.0 / Hc[c];
-      for (int r = c + 1; r < N; ++r) Hc[r] *= inv;
-    }
-    for (int j = 0; j < N; ++j) {              // L y = v
-      __syncthreads();
-      const double yj = v[j];
-      const double* Lj = H + cs<N>(j) - j;
-      for (int r = cl; r < N; r += CSTEP)
-        if (r > j) v[r] = fma(-Lj[r], yj, v[r]);
-    }
-    __syncthreads();
-    for (int r = cl; r < N; r += CSTEP) v[r] /= H[cs<N>(r)];
-    for (int j = N - 1; j >= 0; --j) {         // L^T x = D^-1 y
-      __syncthreads();
-      const double xj = v[j];
-      for (int c = cl; c < N; c += CSTEP)
-        if (c < j) v[c] = fma(-(H + cs<N>(c) - c)[j], xj, v[c]);
-    }
-    __syncthreads();
-  }
-}
-
-// Register-resident solve of the two blocks of a query (N = Ds <= 64): lane c holds column c
-// of the symmetric block (all N rows) and runs a fully unrolled right-looking LDL^T; with
-// 2N <= 64 both blocks run at once in the two 32-lane halves.  Step j needs the pivot
-// column A[r][j], r >= j -- by symmetry lane r's own col[j] -- in every lane: each lane
-// publishes col[j] to an LDS slot (one ds_write per lane) and the column comes back as
-// uniform-address reads (LDS broadcasts, two rows per ds_read_b128), consumed right away
-// by the rank-1 update.  (A v_readlane / ds_bpermute per element costs N^2/2 serialised
-// broadcasts: NCF k=16 spent 0.84 ms of 0.95 there.)  After step j lane c > j keeps
-// L[c][j] in col[j] (forward solve) and its own column below the diagonal holds
-// d_c L[r][c] (backward solve).  The forward solve L y = g rides along (lane j publishes
-// y_j with the pivot column); the backward solve broadcasts one value per step
-// by v_readlane.  g: right-hand sides [2N] (LDS), v: solutions [2N] (LDS),
-// P: pivot-column staging [68] (LDS).
-template <int N>
-__device__ __forceinline__ double bcast_col(double x, int j) {
-  if constexpr (2 * N <= 64) {
-    const double lo = readlane_d(x, j), hi = readlane_d(x, 32 + j);
-    return (threadIdx.x & 32) ? hi : lo;
-  } else {
-    return readlane_d(x, j);
-  }
-}
-
-
-template <class M>
-__device__ void solve_blocks_regs(const double* __restrict__ Gu, const double* __restrict__ Gi, double s2n,
-                                  double wd, double damping, const double* __restrict__ g, double* __restrict__ v,
-                                  double* __restrict__ Hs, double* __restrict__ P) {
-  constexpr int N = M::Ds, GS = N * (N + 1) / 2;
-  // N = 65 (MF k=64: 64 embedding coordinates + the bias): the 64 lanes own columns 0..63
-  // and the bias coordinate rides along -- its row is the last entry of every column, its
-  // pivot-row entry is published by the pivot lane, and its own diagonal and right-hand
-  // side are carried redundantly by every lane (a Schur complement, one step per column)
-  constexpr bool EXTRA = N == 65;
-  constexpr int NC = EXTRA ? 64 : N;            // lane-owned columns
-  static_assert(N <= 65, "one column per lane (+ the MF bias)");
-  constexpr bool PAR = 2 * N <= 64;
-  // lane-derived values are made opaque where they are used, so the compiler does not
-  // hoist N column addresses and N lane masks out of the caller's query loop (spills)
-  int lane = threadIdx.x;
-  asm volatile("" : "+v"(lane));
-  // D_s <= 33: the columns come straight from the cached blocks (L2) -- for a fixed row r
-  // the lanes c < r read consecutive words of packed row r, the lanes c >= r their own row
-  // c (yelp-ex NCF k=16 solve 0.48 -> 0.41 ms); larger blocks are staged through LDS with
-  // coalesced loads first (MF k=64: 1.27 vs 1.49 ms direct)
-  constexpr bool DIRECT = N <= 33;
-  if constexpr (!DIRECT) {
-    for (int t = lane; t < GS; t += kSolveThreads) {
-      Hs[t] = Gu[t];
-      Hs[GS + t] = Gi[t];
-    }
-    __syncthreads();
-  }
-#pragma unroll 1
-  for (int b0 = 0; b0 < (PAR ? 1 : 2); ++b0) {
-    const int b = PAR ? lane >> 5 : b0;
-    const int c = PAR ? lane & 31 : lane;
-    const bool live = c < NC;
-    const double* __restrict__ Gb = DIRECT ? (b ? Gi : Gu) : Hs + b * GS;
-    // column slots (one per lane of the block) + y_j + a dummy slot; every lane publishes.
-    // PAR: the halves use [0, 34) and [34, 68); otherwise the blocks run in turn on [0, 66)
-    // (EXTRA: [0, 68) with the bias row entry at 64 and y_j at 66)
-    constexpr int XS = 64;
-    constexpr int YS = EXTRA ? 66 : PAR ? 32 : 64;
-    double* __restrict__ Pb = P + (PAR ? b * 34 : 0);
-    double col[N];
-#pragma unroll
-    for (int r = 0; r < N; ++r) {
-      const int hi = r > c ? r : c, lo = r > c ? c : r;
-      col[r] = live ? s2n * Gb[gidx<M>(hi, lo)] : 0.0;
-    }
-#pragma unroll
-    for (int r = 0; r < N; ++r)
-      if (r == c) col[r] += (M::decayed(r) ? wd : 0.0) + damping;
-    double y = live ? g[b * N + c] : 0.0;
-    double dinv_own = 0.0;
-    // EXTRA: the bias coordinate's pivot and right-hand side (identical in every lane)
-    double d_x = EXTRA ? s2n * Gb[gidx<M>(N - 1, N - 1)] + (M::decayed(N - 1) ? wd : 0.0) + damping : 0.0;
-    double y_x = EXTRA ? g[b * N + N - 1] : 0.0;
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      Pb[c] = col[j];                           // A[c][j] (= col[j] by symmetry); rows >= j read
-      Pb[c == j ? YS : YS + 1] = y;             // y_j is final: the forward solve rides along
-                                                // (slot YS + 1: the other lanes' unconditional store)
-      if constexpr (EXTRA) Pb[c == j ? XS : XS + 1] = col[N - 1];   // A[bias][j]
-      wave_lds_sync();
-      const double dj = Pb[j];
-      double ij = __builtin_amdgcn_rcp(dj);     // 1/d_j: v_rcp_f64 + two Newton steps
-      ij = fma(ij, fma(-dj, ij, 1.0), ij);
-      ij = fma(ij, fma(-dj, ij, 1.0), ij);
-      if (c == j) dinv_own = ij;
-      const double f = c > j ? col[j] * ij : 0.0;
-      const double yj = Pb[YS];
-      y = fma(-f, yj, y);                       // L y = g, column j
-      // fixed trip count: the inner loop unrolls before the outer one, so a j-dependent
-      // bound would leave col[] indexed at run time (scratch)
-#pragma unroll
-      for (int r = 0; r < NC; ++r)
-        if (r > j) col[r] = fma(-Pb[r], f, col[r]);
-      if constexpr (EXTRA) {
-        const double ax = Pb[XS];
-        col[N - 1] = fma(-ax, f, col[N - 1]);
-        const double lx = ax * ij;              // L[bias][j]
-        d_x = fma(-lx, ax, d_x);
-        y_x = fma(-lx, yj, y_x);
-      }
-      if (c > j) col[j] = f;
-      wave_lds_sync();                          // this step's reads before the next writes
-    }
-    y *= dinv_own;
-    if constexpr (EXTRA) {                      // bias solution, then its column of L^T
-      const double xx = y_x / d_x;
-      y = fma(-col[N - 1] * dinv_own, xx, y);
-      if (lane == 0) v[b * N + N - 1] = xx;
-    }
-#pragma unroll
-    for (int j = NC - 1; j >= 0; --j) {       // L^T x = D^-1 y
-      const double xj = bcast_col<N>(y, j);
-      if (c < j) y = fma(-col[j] * dinv_own, xj, y);
-    }
-    if (live) v[b * N + c] = y;
-  }
-  __syncthreads();
-}
-
 __device__ __forceinline__ double wave_sum(double x) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
@@ -405,18 +223,15 @@ __device__ void solve_epilogue(const QueryArgs& A, int64_t q, int32_t u, int32_t
   }
 }
 
-// One wave per query.  COLS: the two blocks of a query whose test pair is not a train row
-// are solved by ldlt_cols (the path for NCF and MF k >= 32); queries whose pair IS a train
-// row (coupled blocks) are appended to `coupled` {count, q...} for the full-D launch.
-// !COLS: the full D x D packed LDL^T (coupled queries, or every query of qlist).
-// qlist (nullable): {count, q_0, q_1, ...}.
-template <class M, bool COLS>
+// One wave per query, the full D x D packed LDL^T: the queries whose test pair is a train row
+// (its Hessian couples the user and item blocks; the side-system solves list them in qlist
+// {count, q_0, q_1, ...}).
+template <class M>
 __global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist,
-                                                         int32_t* __restrict__ coupled_out) {
+                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
-  __shared__ double H[COLS ? 2 * GS : D * (D + 1) / 2];
-  __shared__ double v[D], g[D], th[D], dd[D], ww[D], pv[68];
+  __shared__ double H[D * (D + 1) / 2];
+  __shared__ double v[D], g[D], th[D], dd[D], ww[D];
   __shared__ double sh[4 * K + 8];
   // NCF weights staged once per block (fp64), read by every query the block solves
   __shared__ NCFWeights<M::ncf ? K : 2> w;
@@ -457,32 +272,7 @@ __global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(
   // ---- assemble H and solve ----
   const double* Gu = A.gram[0] + (int64_t)u * ((GS + 1) & ~1);
   const double* Gi = A.gram[1] + (int64_t)i * ((GS + 1) & ~1);
-  if constexpr (COLS) {
-    if (coupled) {
-      if (lane == 0) {
-        const int slot = atomicAdd(coupled_out, 1);
-        coupled_out[1 + slot] = (int32_t)q;
-      }
-      continue;
-    }
-    if constexpr (M::Ds <= 65) {
-      solve_blocks_regs<M>(Gu, Gi, s2n, A.wd, A.damping, g, v, H, pv);
-    } else {
-      // block b: H_b = (2/n) Gram_b + wd on decayed coordinates + damping, column-major
-      for (int t = lane; t < 2 * GS; t += kSolveThreads) {
-        const int b = t >= GS, tt = t - b * GS;
-        int r = (int)((sqrt(8.0 * tt + 1.0) - 1.0) * 0.5);
-        while (tri(r + 1, 0) <= tt) ++r;
-        while (tri(r, 0) > tt) --r;
-        const int c = tt - tri(r, 0);
-        double h = s2n * (b ? Gi : Gu)[tt];
-        if (r == c) h += (M::decayed(r) ? A.wd : 0.0) + A.damping;
-        H[b * GS + cs<Ds>(c) + (r - c)] = h;
-      }
-      for (int a = lane; a < D; a += kSolveThreads) v[a] = g[a];
-      ldlt_cols<Ds>(H, v);
-    }
-  } else {
+  {
     for (int t = lane; t < D * (D + 1) / 2; t += kSolveThreads) {
       int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
       while (tri(r + 1, 0) <= t) ++r;
@@ -616,11 +406,7 @@ __device__ __forceinline__ double col_sum4(double x) {
 // waves per SIMD the tile solve is compiled for (registers: 4 tiles of state per 16 coordinates)
 template <class M>
 constexpr int col_waves() {
-#ifdef FIA_COL_WAVES
-  return M::Ds <= 16 ? 4 : FIA_COL_WAVES;
-#else
   return M::Ds <= 16 ? 4 : 2;     // N = 32: two 32-row columns per lane (128 VGPRs of matrix)
-#endif
 }
 
 template <class M>
@@ -1102,20 +888,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
   for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
   for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
   const int64_t stride = (int64_t)gridDim.x * QW;
-#ifdef FIA_STAMPS
-  long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long t_prev = __builtin_amdgcn_s_memtime();
-  int iters = 0;
-#define STAMP(k) do { const long long t_ = __builtin_amdgcn_s_memtime(); st[k] += t_ - t_prev; t_prev = t_; } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#endif
   for (int64_t q0 = (int64_t)blockIdx.x * QW; q0 < Q; q0 += stride) {
     __syncthreads();
-#ifdef FIA_STAMPS
-    ++iters;
-#endif
-    STAMP(0);
     // lane-derived values made opaque per iteration: hoisted out of the loop, the 2N column
     // addresses and lane masks would stay live across it (spills)
     int lane = threadIdx.x;
@@ -1136,13 +910,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
       s_n[lane] = nn;
     }
     wave_lds_sync();
-    STAMP(1);
     const int32_t ent = sd ? s_i[qs] : s_u[qs];
     const double* __restrict__ Gb = A.gram[sd] + (int64_t)ent * GSP;
     const int ca = t, cb = t + LS;
     // the prologue first: holding the 2N loaded columns across it spills
     ncf_prologue_multi<M, QW>(A, s_u, s_i, th, g, sh, w, sW1, sb1, rh);
-    STAMP(2);
     double c0[N], c1[N];
 #pragma unroll
     for (int r = 0; r < N; ++r) {
@@ -1168,18 +940,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
     double y0 = g[qs][sd * N + ca], y1 = g[qs][sd * N + cb];
     const double g0 = y0, g1 = y1;
     ncf2_publish<N, 0>(c0, c1, y0, y1, t, &Pv[0][sys * PSTR]);
-#ifdef FIA_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("" : "+v"(c0[N - 1]), "+v"(c1[N - 1]));
-#endif
-    STAMP(3);
     double di0 = 0.0, di1 = 0.0;
     ncf2_steps<N, 0>(c0, c1, y0, y1, di0, di1, t, &Pv[0][sys * PSTR], &Pv[1][sys * PSTR]);
-    STAMP(4);
     y0 *= di0;
     y1 *= di1;
     ncf2_back<N, N - 1>(c0, c1, y0, y1, di0, di1, t);
-    STAMP(5);
     if (lane < QW) {                                 // is the test pair a train row?
       double cdup, rsum;
       A.pairs.probe_finish(pk, ph, pv, cdup, rsum);
@@ -1227,14 +992,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
         coupled_out[1 + slot] = (int32_t)q;
       }
     }
-    STAMP(6);
   }
-#ifdef FIA_STAMPS
-  if (threadIdx.x == 0 && (blockIdx.x % 512) == 0)
-    printf("stamps blk %d iters %d: ids %lld prologue %lld loads %lld elim %lld back %lld epi %lld loop %lld\n",
-           (int)blockIdx.x, iters, st[1], st[2], st[3], st[4], st[5], st[6], st[0]);
-#endif
-#undef STAMP
 }
 
 // ------------------------------------------------------------------------------------
@@ -1243,7 +1001,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
 //    v = d r-hat / d theta_t in block order (ncf:102-145, 181-191; gnn:155) into
 //    qpro[q] = {v[D] | r-hat, n, c_dup, 0}.  The MLP is ~0.8 k FMAs per query; computed
 //    wave-cooperatively inside the solve (k_solve_col) it took a fifth of that kernel
-//    (LDS round trips between tiny loops, FIA_STAMPS).
+//    (LDS round trips between tiny loops, by s_memtime stamps of a diagnostic build).
 //  k_solve_rows: 16 lanes per side system (4 systems = 2 queries per wave); lane t owns rows
 //    t and 31 - t of the lower triangle, 33 entries, loaded from the Gram's row-pair layout
 //    (gidx: one 128-B line per slot and system).  Right-looking LDL^T: step J publishes the
@@ -1256,13 +1014,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
 // ------------------------------------------------------------------------------------
 template <class M>
 constexpr int qpro_stride() { return M::D + 4; }
-#ifndef FIA_ROWS_RG
-#define FIA_ROWS_RG 8
-#endif
-#ifndef FIA_ROWS_WAVES
-#define FIA_ROWS_WAVES 2      // 198 VGPRs, no spills; at 3 waves (168 VGPRs) 34 spill: 0.252 vs 0.220 ms at yelp-ex
-#endif
-constexpr int kRowsRG = FIA_ROWS_RG;      // pivot reads per group (A/B build knob)
+constexpr int kRowsRG = 8;         // pivot reads per group
+constexpr int kRowsWaves = 2;      // 198 VGPRs, no spills; at 3 waves (168 VGPRs) 34 spill: 0.252 vs 0.220 ms at yelp-ex
 
 template <class M>
 __global__ __launch_bounds__(256) void k_ncf_query_pro(QueryArgs A, int64_t Q, double* __restrict__ qpro) {
@@ -1437,7 +1190,7 @@ __device__ __forceinline__ void rows_back(const double (&a)[16], const double (&
 }
 
 template <class M>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FIA_ROWS_WAVES))) void k_solve_rows(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRowsWaves))) void k_solve_rows(
     QueryArgs A, int64_t Q, const double* __restrict__ qpro, double* __restrict__ rec, double* __restrict__ x_out,
     int32_t* __restrict__ coupled_out) {
   static_assert(pair_layout<M>(), "NCF k = 16 (side blocks of 32)");
@@ -2068,348 +1821,15 @@ __global__ __launch_bounds__(256) void k_gram_combine(int64_t n_comb0, const int
 // of every chunk (|influence| desc, position asc) go to its candidate slots.
 // ------------------------------------------------------------------------------------
 
-// waves per SIMD the headline kernel is compiled for (A/B: -DFIA_SCORE_WAVES=5 spills 68 B/lane)
-#ifndef FIA_SCORE_WAVES
-#define FIA_SCORE_WAVES 4
-#endif
-template <class M>
-__global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(FIA_SCORE_WAVES))) void k_score_mf(
-    QueryArgs A, int64_t Q, const int64_t* __restrict__ coff, const ChunkDesc* __restrict__ cdesc,
-    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
-    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf, "MF scoring");
-  constexpr int K = M::K, RT = kScoreRows, NV = (M::SB + 63) / 64;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nchunks = coff[Q];
-  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  struct Stage {
-    ChunkDesc d;
-    int32_t o[RT], row[RT];
-    float y[RT];
-    double hv, rv[NV];
-  };
-  auto fetch = [&](int64_t c, Stage& st) {
-    st.d = cdesc[c];
-    const int sd = st.d.side;
-    const int32_t* __restrict__ oth = A.other[sd] + st.d.list_base;
-    const float* __restrict__ rat = A.rating[sd] + st.d.list_base;
-    const int32_t* __restrict__ rw = A.row[sd] + st.d.list_base;
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int idx = r * 64 + lane;
-      const int li = idx < st.d.len ? idx : 0;
-      st.o[r] = oth[li];
-      st.y[r] = rat[li];
-      st.row[r] = rw[li];
-    }
-    const double* __restrict__ R = rec + (int64_t)st.d.q * M::R;
-    const double* __restrict__ Sg = R + 4 + sd * M::SB;
-    st.hv = R[lane & 3];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) st.rv[v] = Sg[v * 64 + lane < M::SB ? v * 64 + lane : M::SB - 1];
-  };
-  int64_t ch = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave;
-  Stage cur;
-  if (ch < nchunks) fetch(ch, cur);
-  while (ch < nchunks) {
-    const int sd = cur.d.side;
-    // gathers of the current chunk
-    float4 g4_[RT][K / 4];
-    float gb_[RT];
-    {
-      const float* T = sd == 0 ? A.t[1] : A.t[0];
-      const float* bt = sd == 0 ? A.t[3] : A.t[2];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const float4* src = reinterpret_cast<const float4*>(T + (int64_t)cur.o[r] * K);
-#pragma unroll
-        for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
-        gb_[r] = bt[cur.o[r]];
-      }
-    }
-    // next chunk's descriptor, list entries and record, behind the gathers
-    const int64_t nx = ch + stride;
-    Stage nxt;
-    if (nx < nchunks) fetch(nx, nxt);
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-#pragma unroll
-      for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
-      asm volatile("" ::"v"(gb_[r]));
-    }
-    const ChunkDesc& d = cur.d;
-    const double inv_n = readlane_d(cur.hv, 0), cq = readlane_d(cur.hv, 1), xv = readlane_d(cur.hv, 2),
-                 rhat_ui = readlane_d(cur.hv, 3);
-#define RS(c) readlane_d(cur.rv[(c) / 64], (c) % 64)
-    double dot_a[RT], dot_x[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) dot_a[r] = dot_x[r] = 0.0;
-#pragma unroll
-    for (int c4 = 0; c4 < K / 4; ++c4) {
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const double ac = RS(4 * c4 + cc), xc = RS(K + 4 * c4 + cc);
-#pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          const float4 t = g4_[r][c4];
-          const double tv = (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w);
-          dot_a[r] = fma(ac, tv, dot_a[r]);
-          dot_x[r] = fma(xc, tv, dot_x[r]);
-        }
-      }
-    }
-    const double bias_s = RS(2 * K), xsb = RS(2 * K + 1), dup_o = RS(2 * K + 2);
-#undef RS
-    double ca[RT], cv[RT];
-    int cp[RT];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const int idx = r * 64 + lane;
-      const bool ok = idx < d.len;
-      const double y = (double)cur.y[r];
-      double e = dot_a[r] + bias_s + (double)gb_[r] - y;
-      double s = dot_x[r] + xsb;
-      if ((double)cur.o[r] == dup_o) { e = rhat_ui - y; s = xv; }
-      const double infl = (2.0 * e * s + cq) * inv_n;
-      if (ok) {
-        if (influence) __builtin_nontemporal_store(infl, influence + d.out_base + idx);
-        if (rel_idx) __builtin_nontemporal_store(cur.row[r], rel_idx + d.out_base + idx);
-      }
-      cp[r] = ok ? d.pos0 + idx : -1;
-      ca[r] = ok ? topk_key(infl) : -2.0;
-      cv[r] = infl;
-    }
-    if (K_top > 0) {
-      double pa = INFINITY;
-      int pp = -1;
-      for (int t = 0; t < K_top; ++t) {
-        double ba = -2.0, bv = 0.0;
-        int bp = 0x7fffffff;
-#pragma unroll
-        for (int r = 0; r < RT; ++r)
-          if (cp[r] >= 0 && better(pa, pp, ca[r], cp[r]) && better(ca[r], cp[r], ba, bp)) {
-            ba = ca[r]; bp = cp[r]; bv = cv[r];
-          }
-        wave_best(ba, bp, bv);
-        if (lane == 0) {
-          const bool okk = ba > -1.5;
-          cand_pos[ch * K_top + t] = okk ? bp : -1;
-          cand_val[ch * K_top + t] = okk ? bv : NAN;
-        }
-        pa = ba;
-        pp = bp;
-      }
-    }
-    cur = nxt;
-    ch = nx;
-  }
-}
-
 // ------------------------------------------------------------------------------------
-// Entity-shared scoring.  A work item is one chunk (<= kChunk ratings) of ONE entity's
-// list (user list R_u or item list C_i) together with every query of the batch that
-// has that entity.  The list entries, the gathered other-side embedding rows and the
-// per-rating residual e_j = r-hat_j - y_j depend on the train rating only, so they are
-// loaded / computed once per work item and reused for every query in the group; per query only s_jq = x_q . g_j is
-// new.  influence_jq = (2 e_j s_jq + c_q) / n_q  (mf:240-246).  The test pair's own
-// train row takes e and s from the query record (bit-identical copies, see k_solve).
-// ------------------------------------------------------------------------------------
-// rows per lane per scoring pass (register budget of the gathered rows / NCF backward
-// vectors); kScoreRows / score_rw passes per work item, one candidate slot set each
-template <class M>
-constexpr int score_rw() {
-  return M::K >= 64 ? 1 : M::K >= 32 ? 2 : 4;
-}
-
-template <class M>
-__global__ __launch_bounds__(kScoreThreads) void k_score_grouped(
-    QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
-    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
-    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf, "MF scoring (NCF: k_score_ncf)");
-  constexpr int K = M::K;
-  constexpr int RT = kScoreRows;                 // rows per lane per work item
-  constexpr int RW = score_rw<M>();              // rows per lane per pass
-  constexpr int NPASS = RT / RW;
-  constexpr int NSV = (K + 1 + 63) / 64;         // entity words per lane
-  constexpr int QB = kQueryBlock;
-  constexpr int RSW = 4 + M::SB;                  // staged record words: header + this side's block
-  // per wave: the query block's records (uniform-address reads = LDS broadcasts) and
-  // per query {output base, candidate-slot base, position offset}
-  __shared__ double srec[kScoreThreads / 64][QB * RSW];
-  __shared__ int64_t sbase[kScoreThreads / 64][3 * QB];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t n_items = wstart[nE];
-  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
-    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
-    const int sd = g >= A.U ? 1 : 0;
-    const int32_t e = sd ? (int32_t)(g - A.U) : g;
-    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
-    const int64_t rem = A.ptr[sd][e + 1] - lb;
-    const int len = rem < kChunk ? (int)rem : kChunk;
-    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
-    const int64_t gn = gstart[g + 1] - gb;
-    const int nq = gn < QB ? (int)gn : QB;
-    const int32_t* __restrict__ oth = A.other[sd] + lb;
-    const float* __restrict__ rat = A.rating[sd] + lb;
-    const int32_t* __restrict__ rw = A.row[sd] + lb;
-    // the entity's own embedding + bias, spread over lanes
-    double selfv[NSV];
-#pragma unroll
-    for (int v = 0; v < NSV; ++v) {
-      const int c = v * 64 + lane;
-      const float* Es = sd == 0 ? A.t[0] : A.t[1];
-      const float* Bs = sd == 0 ? A.t[2] : A.t[3];
-      selfv[v] = c < K ? (double)Es[(int64_t)e * K + c] : (double)Bs[e];
-    }
-#define SV(c) readlane_d(selfv[(c) / 64], (c) % 64)
-    // stage the query block (queries past the group end repeat the last one; never used)
-    double* __restrict__ rl = srec[wave];
-    int64_t* __restrict__ bl = sbase[wave];
-    __builtin_amdgcn_wave_barrier();
-    for (int t = lane; t < QB * RSW; t += 64) {
-      const int j = t / RSW, c = t - j * RSW;
-      const int32_t q = gq[gb + (j < nq ? j : nq - 1)];
-      rl[t] = rec[(int64_t)q * M::R + (c < 4 ? c : 4 + sd * M::SB + (c - 4))];
-    }
-    if (lane < QB) {
-      const int32_t q = gq[gb + (lane < nq ? lane : nq - 1)];
-      const int64_t* qb = qbase + 4 * (int64_t)q;
-      bl[lane] = qb[sd] + (int64_t)cidx * kChunk;
-      bl[QB + lane] = qb[2 + sd] + cidx;
-      bl[2 * QB + lane] = sd ? qb[1] - qb[0] : 0;   // |R_u| precedes item-side positions
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int h = 0; h < NPASS; ++h) {
-      int32_t o_[RW], row_[RW];
-      float y_[RW];
-      bool ok_[RW];
-#pragma unroll
-      for (int r = 0; r < RW; ++r) {
-        const int idx = (h * RW + r) * 64 + lane;
-        ok_[r] = idx < len;
-        const int li = ok_[r] ? idx : 0;
-        o_[r] = oth[li];
-        y_[r] = rat[li];
-        row_[r] = rw[li];
-      }
-#pragma unroll
-      for (int r = 0; r < RW; ++r) asm volatile("" ::"v"(o_[r]), "v"(row_[r]), "v"(y_[r]));
-      // per-rating quantities shared by the whole query block
-      float4 g4_[RW][(K + 3) / 4];               // other-side embedding row
-      double ej[RW];                             // residual r-hat_j - y_j
-      {
-        const float* T = sd == 0 ? A.t[1] : A.t[0];
-        float gb_[RW];
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          const float4* src = reinterpret_cast<const float4*>(T + (int64_t)o_[r] * K);
-#pragma unroll
-          for (int c = 0; c < K / 4; ++c) g4_[r][c] = src[c];
-          gb_[r] = (sd == 0 ? A.t[3] : A.t[2])[o_[r]];
-        }
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-#pragma unroll
-          for (int c = 0; c < K / 4; ++c) asm volatile("" ::"v"(g4_[r][c].x), "v"(g4_[r][c].w));
-        }
-        const double gbias = (double)A.t[4][0];
-        const double bself = SV(K);
-#pragma unroll
-        for (int r = 0; r < RW; ++r) ej[r] = 0.0;
-#pragma unroll
-        for (int c4 = 0; c4 < K / 4; ++c4)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            const double pc = SV(4 * c4 + cc);
-#pragma unroll
-            for (int r = 0; r < RW; ++r) {
-              const float4 t = g4_[r][c4];
-              ej[r] = fma(pc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), ej[r]);
-            }
-          }
-#pragma unroll
-        for (int r = 0; r < RW; ++r) ej[r] = ej[r] + bself + (double)gb_[r] + gbias - (double)y_[r];
-      }
-      // every query of the block: s_jq = x_q . g_j, then influence, outputs, candidates
-#pragma unroll 1
-      for (int j = 0; j < nq; ++j) {
-        const double* __restrict__ Rj = rl + j * RSW;
-#define RS(cc) Rj[4 + (cc)]
-        const double inv_n = Rj[0], cq = Rj[1], xv = Rj[2], rhat_ui = Rj[3];
-        const int64_t obj = bl[j], cbj = bl[QB + j], poj = bl[2 * QB + j];
-        double sj[RW];
-#pragma unroll
-        for (int r = 0; r < RW; ++r) sj[r] = 0.0;
-#pragma unroll
-        for (int c4 = 0; c4 < K / 4; ++c4)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            const double xc = RS(K + 4 * c4 + cc);
-#pragma unroll
-            for (int r = 0; r < RW; ++r) {
-              const float4 t = g4_[r][c4];
-              sj[r] = fma(xc, (double)(cc == 0 ? t.x : cc == 1 ? t.y : cc == 2 ? t.z : t.w), sj[r]);
-            }
-          }
-        const double xsb = RS(2 * K + 1);
-#pragma unroll
-        for (int r = 0; r < RW; ++r) sj[r] += xsb;
-        const double dup_o = RS(2 * K + 2);
-#undef RS
-        double la[RW], lv[RW];
-        int lp[RW];
-#pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          double ee = ej[r], ss = sj[r];
-          if ((double)o_[r] == dup_o) { ee = rhat_ui - (double)y_[r]; ss = xv; }
-          const double infl = (2.0 * ee * ss + cq) * inv_n;
-          const int idx = (h * RW + r) * 64 + lane;
-          if (ok_[r]) {   // streaming outputs: nontemporal, so they do not evict the gathered tables from L2
-            if (influence) __builtin_nontemporal_store(infl, influence + obj + idx);
-            if (rel_idx) __builtin_nontemporal_store(row_[r], rel_idx + obj + idx);
-          }
-          lp[r] = ok_[r] ? cidx * kChunk + idx : -1;    // related position inside this side's list
-          la[r] = ok_[r] ? topk_key(infl) : -2.0;
-          lv[r] = infl;
-        }
-        if (K_top > 0) {
-          // pass h's candidates for this query; k_topk_merge merges the NPASS slot sets of
-          // every chunk: slot (chunk c, pass h) -> c * NPASS + h
-          double pa = INFINITY;
-          int pp = -1;
-          for (int t = 0; t < K_top; ++t) {
-            double ba = -2.0, bv = 0.0;
-            int bp = 0x7fffffff;
-#pragma unroll
-            for (int r = 0; r < RW; ++r)
-              if (lp[r] >= 0 && better(pa, pp, la[r], lp[r]) && better(la[r], lp[r], ba, bp)) {
-                ba = la[r]; bp = lp[r]; bv = lv[r];
-              }
-            wave_best(ba, bp, bv);
-            if (lane == 0) {
-              const bool okk = ba > -1.5;
-              const int64_t slot = (cbj * NPASS + h) * K_top + t;
-              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
-              cand_val[slot] = okk ? bv : NAN;
-            }
-            pa = ba;
-            pp = bp;
-          }
-        }
-      }
-    }
-#undef SV
-    __builtin_amdgcn_wave_barrier();   // staged block fully consumed before the next item overwrites it
-  }
-}
+// Entity-shared scoring (MF k >= 32, NCF).  A work item is one chunk (<= kChunk ratings) of
+// ONE entity's list (user list R_u or item list C_i) together with a block of the batch's
+// queries that have that entity.  The list entries, the gathered other-side embedding rows
+// and the per-rating residual e_j = r-hat_j - y_j depend on the train rating only, so they
+// are loaded / computed once per work item and reused for every query in the block; per
+// query only s_jq = x_q . g_j is new.  influence_jq = (2 e_j s_jq + c_q) / n_q
+// (mf:240-246).  The test pair's own train row takes e and s from the query record
+// (bit-identical copies, see k_solve).
 
 // ------------------------------------------------------------------------------------
 // MF k >= 32 entity-shared scoring with the query vectors read through the scalar cache.
@@ -2614,21 +2034,14 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
 // ------------------------------------------------------------------------------------
 constexpr int kMfmaQB = 15;   // queries per work item (row 15 of A is the entity)
 constexpr int kMfmaCPI = 4;   // list chunks (256 ratings) per work item: the item's setup loads amortised
-#ifndef FIA_MFMA_RING
-#define FIA_MFMA_RING 3
-#endif
-constexpr int kMfmaRing = FIA_MFMA_RING;   // tiles in flight (A/B build knob: 3 or 4)
+constexpr int kMfmaRing = 3;   // tiles in flight (a fourth slot spills at 2 waves per SIMD: 3.26 vs 3.12 ms)
 
 // output stores of k_score_mf_mfma: 128-B runs of one query per 16 lanes, at the query's
 // arbitrary 8-B alignment; plain stores keep the straddled L2 lines until the next tile
 // completes them
 template <class T>
 __device__ __forceinline__ void st_out(T v, T* p) {
-#ifdef FIA_MFMA_NT_STORES
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 // every lane gets lane 48 + (l & 15)'s value (row 3 of a 16x16 f64 MFMA C register, column
@@ -2666,13 +2079,14 @@ __device__ __forceinline__ long long topk_ikey(double v) {
   return b > 0x7ff0000000000000ll ? -1ll : b;
 }
 
-template <class M, bool FULL, int CPI, int SETUP>
+template <class M, bool FULL>
 __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_score_mf_mfma(
     QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  static_assert(!M::ncf && (M::K == 16 || M::K == 32 || M::K == 64), "MF k in {16, 32, 64}");
+  constexpr int CPI = kMfmaCPI;
+  static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
   constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, TPC = kChunk / 16;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2701,26 +2115,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
     const double bself = (double)(sd == 0 ? A.t[2] : A.t[3])[e];
     // A operand: lane (row cn, group kk) holds coordinates KS*kk .. KS*kk+KS-1 of its row
     double a[KS];
-    if constexpr (SETUP >= 2) {
-      // unconditional loads (clamped indices, selects after)
-      const int32_t qa = gq[gb + (cn < nq ? cn : nq - 1)];
-      const double2* srcx = reinterpret_cast<const double2*>(rec + (int64_t)qa * M::R + 4 + sd * M::SB + K + KS * kk);
-      const float4* srce = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
-      double2 xv[KS / 2];
-      float4 ev[NF4];
-#pragma unroll
-      for (int f = 0; f < KS / 2; ++f) xv[f] = srcx[f];
-#pragma unroll
-      for (int f = 0; f < NF4; ++f) ev[f] = srce[f];
-      const bool self_row = cn == 15;
-#pragma unroll
-      for (int f = 0; f < NF4; ++f) {
-        a[4 * f + 0] = self_row ? (double)ev[f].x : xv[2 * f].x;
-        a[4 * f + 1] = self_row ? (double)ev[f].y : xv[2 * f].y;
-        a[4 * f + 2] = self_row ? (double)ev[f].z : xv[2 * f + 1].x;
-        a[4 * f + 3] = self_row ? (double)ev[f].w : xv[2 * f + 1].y;
-      }
-    } else if (cn == 15) {
+    if (cn == 15) {
       const float4* src = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
 #pragma unroll
       for (int f = 0; f < NF4; ++f) {
@@ -2744,7 +2139,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
     int dl[4] = {0, 0, 0, 0};         // misalignment of each query row's output run (elements)
     int64_t cslot[4];
     bool qv[4];
-    if constexpr (SETUP >= 1) {
+    {
       // every query index first, then every per-query load (one wait)
       int32_t qr[4];
 #pragma unroll
@@ -2767,43 +2162,11 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         const int64_t ob = (sd ? q01.y : q01.x) + p0 + cn;
         cslot[r] = (sd ? q23.y : q23.x) + (int64_t)cg * CPI;
         cpos[r] = (int32_t)(p0 + sd * (q01.y - q01.x));
-#ifndef FIA_MFMA_NO_ROT
         // aligned stores: the run starts dl elements into a 16-element (128-B influence,
-        // 64-B train-row) segment; lane cn stores segment element cn.  (-DFIA_MFMA_NO_ROT:
-        // plain per-tile stores, same outputs; same-box A/B at 20M MF k=64: 3.03 ms per
-        // batch vs 3.13 ms rotated)
+        // 64-B train-row) segment; lane cn stores segment element cn
         dl[r] = (int)((ob - cn) & 15);
         outp[r] = influence + (ob - cn - dl[r]);   // the aligned segment (lane cn adds cn)
         relp[r] = rel_idx + (ob - cn - dl[r]);
-#else
-        outp[r] = influence + ob;
-        relp[r] = rel_idx + ob;
-#endif
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = kk + 4 * r;
-        qv[r] = m < nq;
-        const int32_t q = gq[gb + (m < nq ? m : 0)];
-        const double* __restrict__ R = rec + (int64_t)q * M::R;
-        const double inv_n = R[0];
-        al[r] = 2.0 * inv_n;
-        be[r] = R[1] * inv_n;
-        xb[r] = R[4 + sd * M::SB + 2 * K + 1];
-        dupo[r] = qv[r] ? (int32_t)R[4 + sd * M::SB + 2 * K + 2] : -1;
-        const int64_t* __restrict__ qb = qbase + 4 * (int64_t)q;
-        const int64_t ob = qb[sd] + p0 + cn;
-        cslot[r] = qb[2 + sd] + (int64_t)cg * CPI;           // candidate slot of the item's first chunk
-        cpos[r] = (int32_t)(p0 + (sd ? qb[1] - qb[0] : 0));  // |R_u| precedes item-side positions
-#ifndef FIA_MFMA_NO_ROT
-        dl[r] = (int)((ob - cn) & 15);
-        outp[r] = influence + (ob - cn - dl[r]);   // the aligned segment (lane cn adds cn)
-        relp[r] = rel_idx + (ob - cn - dl[r]);
-#else
-        outp[r] = influence + ob;
-        relp[r] = rel_idx + ob;
-#endif
       }
     }
     long long bk[4];
@@ -2827,12 +2190,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
       sw[k3] = rw[p];
     };
     auto gather = [&](int k3) {
-#ifdef FIA_ABL_ONE_ROW
-      // ablation (A/B builds only): every gather reads row 0 -- wrong outputs, timing only
-      const float4* row = reinterpret_cast<const float4*>(T + KS * kk);
-#else
       const float4* row = reinterpret_cast<const float4*>(T + (int64_t)so[k3] * K + KS * kk);
-#endif
 #pragma unroll
       for (int f = 0; f < NF4; ++f) sb[k3][f] = row[f];
       sbo[k3] = bt[so[k3]];
@@ -2874,11 +2232,9 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
                      "+v"(bd[6]), "+v"(bd[7]), "+v"(bd[8]), "+v"(bd[9]), "+v"(bd[10]), "+v"(bd[11]),
                      "+v"(bd[12]), "+v"(bd[13]), "+v"(bd[14]), "+v"(bd[15]));
-      else if constexpr (KS == 8)
+      else
         asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
                      "+v"(bd[6]), "+v"(bd[7]));
-      else
-        asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]));
       d4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int sl = 0; sl < KS; ++sl) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sl], bd[sl], acc, 0, 0, 0);
@@ -2911,7 +2267,6 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         bk[r] = take ? key : bk[r];
         bp[r] = take ? p : bp[r];
         bv[r] = take ? val[r] : bv[r];
-#ifndef FIA_MFMA_NO_ROT
         // rotate the row by its misalignment dl: lane cn takes element (cn - dl) & 15 -- of
         // this tile (cn >= dl) or, already rotated, of the previous tile (cn < dl) -- so each
         // store is one aligned 16-element segment (whole lines: no line written twice)
@@ -2920,70 +2275,31 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         const int32_t rw = __shfl(w, srcl);
         const bool cur = cn >= dl[r];
         const int idx = 16 * t + cn - dl[r];          // element of the run this lane stores
-#ifdef FIA_ABL_NO_STORES
-        // ablation (A/B builds only): no output stores -- timing only
-        if (qv[r] && (cur ? idx < len : t > 0) && __double_as_longlong(rv) == 0x7ff8dead0000beefll)
-#else
-        if (qv[r] && (cur ? idx < len : t > 0))
-#endif
-        {
+        if (qv[r] && (cur ? idx < len : t > 0)) {
           if (FULL || influence) st_out(cur ? rv : prv[r], outp[r] + 16 * t + cn);
           if (FULL || rel_idx) st_out(cur ? rw : prw[r], relp[r] + 16 * t + cn);
         }
         prv[r] = rv;
         prw[r] = rw;
-#else
-        if (ok) {
-          if (FULL || influence) st_out(val[r], outp[r] + 16 * t);
-          if (FULL || rel_idx) st_out(w, relp[r] + 16 * t);
-        }
-#endif
       }
       if (t % TPC == TPC - 1 || t == ntl - 1) emit(t / TPC);
     };
-    if constexpr (kMfmaRing == 4) {
-      // ring of four: list entries 3 tiles and rows 2 tiles ahead
-      load_list(0, 0);
-      load_list(1, 1);
-      load_list(2, 2);
-      gather(0);
+    load_list(0, 0);
+    load_list(1, 1);
+    gather(0);
+    for (int t = 0; t < ntl; t += 3) {
+      load_list(t + 2, 2);
       gather(1);
-      for (int t = 0; t < ntl; t += 4) {
-        load_list(t + 3, 3);
-        gather(2);
-        tile(t, 0);
-        if (t + 1 >= ntl) break;
-        load_list(t + 4, 0);
-        gather(3);
-        tile(t + 1, 1);
-        if (t + 2 >= ntl) break;
-        load_list(t + 5, 1);
-        gather(0);
-        tile(t + 2, 2);
-        if (t + 3 >= ntl) break;
-        load_list(t + 6, 2);
-        gather(1);
-        tile(t + 3, 3);
-      }
-    } else {
-      load_list(0, 0);
-      load_list(1, 1);
+      tile(t, 0);
+      if (t + 1 >= ntl) break;
+      load_list(t + 3, 0);
+      gather(2);
+      tile(t + 1, 1);
+      if (t + 2 >= ntl) break;
+      load_list(t + 4, 1);
       gather(0);
-      for (int t = 0; t < ntl; t += 3) {
-        load_list(t + 2, 2);
-        gather(1);
-        tile(t, 0);
-        if (t + 1 >= ntl) break;
-        load_list(t + 3, 0);
-        gather(2);
-        tile(t + 1, 1);
-        if (t + 2 >= ntl) break;
-        load_list(t + 4, 1);
-        gather(0);
-        tile(t + 2, 2);
-      }
+      tile(t + 2, 2);
     }
-#ifndef FIA_MFMA_NO_ROT
     // the run's tail: the last tile's elements past the last aligned segment
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -2993,7 +2309,6 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         if (FULL || rel_idx) st_out(prw[r], relp[r] + 16 * ntl + cn);
       }
     }
-#endif
   }
 }
 
@@ -3368,20 +2683,15 @@ constexpr bool use_col_solve() {
   return M::ncf && 2 * M::Ds <= 64;
 }
 
-// side-system solve (A/B knob FIA_SOLVE): default = k_solve_rows (NCF k = 16) / k_solve_col
-// (NCF k = 8) / k_solve_tile, col = k_solve_col for NCF k = 16, tile = k_solve_tile
-// everywhere, cols = the previous one-column-per-lane k_solve
-static int solve_mode() {
-  static const char* e = getenv("FIA_SOLVE");
-  static const int m = !e ? 0 : !strcmp(e, "cols") ? 1 : !strcmp(e, "tile") ? 2 : !strcmp(e, "col") ? 3 : 0;
-  return m;
+// one side-system solve per model: MF k <= 16 k_solve_tps, NCF k = 16 k_solve_rows, NCF k = 8
+// k_solve_col, MF k in {32, 64} and NCF k = 32 k_solve_tile
+template <class M>
+constexpr bool solve_covered() {
+  return use_tps<M>() || pair_layout<M>() || use_col_solve<M>() || use_tile_solve<M>();
 }
 
-// MF k <= 16 scoring schedule (A/B knob FIA_MF_SCORE): runs (default) | old
-static const char* mf_score_mode() {
-  static const char* m = getenv("FIA_MF_SCORE") ? getenv("FIA_MF_SCORE") : "runs";
-  return m;
-}
+// MF k <= 16 item runs: slice cost target (descriptor cost units per one-wave slice)
+constexpr int kRunLambda = 32;
 
 template <class M>
 hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
@@ -3406,7 +2716,6 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
   {
     int64_t want = 256;
     while (!M::ncf && want < 4096 && want < GSP) want *= 2;   // NCF: 256 (16 slabs per item)
-    want = gram_chunk(want);
     if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want, s));
   }
   const Index& X = c->idx;
@@ -3467,28 +2776,17 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                       int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
                       const double* x_in) {
-  // Auto schedule (measured on MI355X, profiles/): entity-shared scoring wins whenever
-  // the per-rating work is larger than a 64-B gather (k >= 32) -- 20M MF k=64 855 vs
-  // 429 k q/s; for MF k <= 16 the group build costs more than the shared gathers save
-  // (ml-1m-ex 36.6 vs 39.3 M q/s).  NCF scoring is entity-shared only (k_score_ncf).
-  const bool grouped = M::ncf || (c->score_mode >= 0 ? c->score_mode == 1 : M::K >= 32);
-  // MF k in {32, 64} at K <= 1: the f64-MFMA entity-shared kernel (query blocks of 15)
-  constexpr bool mfma_ok = !M::ncf && (M::K == 16 || M::K == 32 || M::K == 64);
-  static const bool mfma_on = !getenv("FIA_NO_MFMA_SCORE");   // A/B knob: k_score_grouped_mf instead
-  const bool use_mfma = mfma_ok && grouped && K <= 1 && mfma_on;
-  // A/B knobs of the MFMA kernel's variants (FIA_MFMA_CPI=1: one chunk per work item;
-  // FIA_MFMA_SETUP=1/2: batched / unconditional work-item setup loads)
-  static const int mfma_cpi = getenv("FIA_MFMA_CPI") ? atoi(getenv("FIA_MFMA_CPI")) : kMfmaCPI;
-  static const int mfma_setup = getenv("FIA_MFMA_SETUP") ? atoi(getenv("FIA_MFMA_SETUP")) : 1;
-  const int cpi_used = (mfma_cpi == 1 && rel_idx && influence) ? 1 : kMfmaCPI;
+  // One scoring schedule per (model, k, K) (measured on MI355X, profiles/): MF k <= 16 item
+  // runs (k_score_mf_runs, per-query chunks sharing the item's list); MF k in {32, 64}
+  // entity-shared, on f64 MFMA for K <= 1 (k_score_mf_mfma, query blocks of 15) and on VALU
+  // otherwise (k_score_grouped_mf); NCF entity-shared (k_score_ncf)
+  constexpr bool grouped = M::ncf || M::K >= 32;
+  constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);
+  const bool use_mfma = mfma_ok && K <= 1;
   const int qblock = use_mfma ? kMfmaQB : query_block<M>();
-  // candidate slot sets per chunk: k_score_grouped writes one per pass
-  constexpr bool one_pass = M::ncf || M::K >= 32;        // k_score_ncf / k_score_grouped_mf
-  // MF k <= 16 per-query chunks: k_score_mf (default) or k_score_mf_run (A/B knob
-  // FIA_MF_SCORE=run), one candidate slot set per chunk
-  const char* mfs = mf_score_mode();
-  const bool runs = !M::ncf && M::K <= 16 && !grouped && strcmp(mfs, "old") != 0;
-  const int spc = grouped && !one_pass ? kScoreRows / score_rw<M>() : 1;
+  constexpr bool runs = !grouped;
+  constexpr int spc = 1;      // candidate slot sets per chunk
+  static_assert(solve_covered<M>(), "every small-k model has a side-system solve");
   FIA_HIP_TRY(c->rec.reserve(sizeof(double) * (size_t)(Q * M::R + 1), s));
   if (K > 0) {
     FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc), s));
@@ -3506,12 +2804,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // costs vary ~10x: a static stride over descriptors left waves idle for half the kernel);
   // the slice count is known on the device only -- the grid is its bound (total cost <=
   // kRunUserCost per descriptor slot), the surplus waves exit at once
-  static const int64_t genv = getenv("FIA_SCORE_GRID") ? atoll(getenv("FIA_SCORE_GRID")) : 0;  // A/B knob
-  static const int lam_env = getenv("FIA_RUNS_LAMBDA") ? atoi(getenv("FIA_RUNS_LAMBDA")) : 0;  // A/B knob
-  const int64_t lam = lam_env > 0 ? lam_env : 32;
+  static const int64_t lam = getenv("FIA_RUNS_LAMBDA") ? atoll(getenv("FIA_RUNS_LAMBDA")) : kRunLambda;  // TEMP A/B
   const int64_t runs_grid = (kRunUserCost * (max_chunks + 1)) / lam + 2;
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam));
-  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? cpi_used : 1));
+  if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
   if (x_in && Q > 0) {
@@ -3523,49 +2819,35 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
   if (Q > 0 && !x_in) {
-    static const bool tps_on = !getenv("FIA_NO_TPS");   // A/B knob: wave-per-query solve instead
-    if (use_tps<M>() && tps_on) {
-      if constexpr (use_tps<M>())
-        hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
-                           c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
-    } else if (pair_layout<M>() && solve_mode() == 0) {
-      if constexpr (pair_layout<M>()) {
-        FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
-        hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(256), 0, s, A, Q,
-                           c->qwork.as<double>());
-        hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
-                           (const double*)c->qwork.as<double>(), c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
-      }
-    } else if (use_col_solve<M>() && (solve_mode() == 0 || solve_mode() == 3)) {
-      if constexpr (use_col_solve<M>()) {
-        static const int64_t genv = getenv("FIA_SOLVE_GRID") ? atoll(getenv("FIA_SOLVE_GRID")) : 0;  // A/B knob
-        const int64_t cap = genv > 0 ? genv : (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;
-        constexpr int QW = 32 / M::K;             // queries per wave
-        const int64_t need = (Q + QW - 1) / QW;
-        const int64_t g1 = need < cap ? need : cap;   // persistent: NCF weights staged once per block
-        hipLaunchKernelGGL(k_solve_col<M>, dim3((unsigned)g1), dim3(64), 0, s, A, Q, c->rec.as<double>(), x_out,
-                           c->coupled.as<int32_t>());
-      }
-    } else if (use_tile_solve<M>() && solve_mode() != 1) {
-      if constexpr (use_tile_solve<M>()) {
-        static const int64_t genv = getenv("FIA_SOLVE_GRID") ? atoll(getenv("FIA_SOLVE_GRID")) : 0;  // A/B knob
-        const int64_t cap = genv > 0 ? genv : (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 8;
-        const int64_t g1 = Q < cap ? Q : cap;     // persistent: NCF weights staged once per block
-        hipLaunchKernelGGL(k_solve_tile<M>, dim3((unsigned)g1), dim3(128), 0, s, A, Q, c->rec.as<double>(), x_out,
-                           c->coupled.as<int32_t>());
-      }
+    if constexpr (use_tps<M>()) {
+      hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
+                         c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+    } else if constexpr (pair_layout<M>()) {
+      FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
+      hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(256), 0, s, A, Q,
+                         c->qwork.as<double>());
+      hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
+                         (const double*)c->qwork.as<double>(), c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
+    } else if constexpr (use_col_solve<M>()) {
+      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 16;
+      constexpr int QW = 32 / M::K;             // queries per wave
+      const int64_t need = (Q + QW - 1) / QW;
+      const int64_t g1 = need < cap ? need : cap;   // persistent: NCF weights staged once per block
+      hipLaunchKernelGGL(k_solve_col<M>, dim3((unsigned)g1), dim3(64), 0, s, A, Q, c->rec.as<double>(), x_out,
+                         c->coupled.as<int32_t>());
     } else {
-      const int64_t g1 = Q < 8192 ? Q : 8192;     // persistent: weights staged once per block
-      hipLaunchKernelGGL((k_solve<M, true>), dim3((unsigned)g1), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
-                         x_out, (const int32_t*)nullptr, c->coupled.as<int32_t>());
+      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 8;
+      const int64_t g1 = Q < cap ? Q : cap;     // persistent: NCF weights staged once per block
+      hipLaunchKernelGGL(k_solve_tile<M>, dim3((unsigned)g1), dim3(128), 0, s, A, Q, c->rec.as<double>(), x_out,
+                         c->coupled.as<int32_t>());
     }
     FIA_HIP_TRY(hipGetLastError());
     // usually no coupled query: a small grid that exits (a full grid for the large full-D
     // systems of k >= 32, should many test pairs be train rows)
     const int64_t gc = M::K <= 16 ? 64 : 256;
     const int64_t g2 = Q < gc ? Q : gc;
-    hipLaunchKernelGGL((k_solve<M, false>), dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(),
-                       x_out, (const int32_t*)c->coupled.as<int32_t>(), (int32_t*)nullptr);
+    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
+                       (const int32_t*)c->coupled.as<int32_t>());
   }
   if constexpr (mask_path<M>()) {
     if (Q > 0) {       // the records' MLP block -> y = W1_side^T x_mlp for k_score_ncf
@@ -3583,7 +2865,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   int64_t grid = (max_items + 3) / 4;            // 4 waves (work items) per block
   if (grid < 1) grid = 1;
   // grid cap (measured): NCF 1024 workgroups (yelp-ex score 0.314 -> 0.290 ms), MF 8192
-  const int64_t gcap = genv > 0 ? genv : M::ncf ? 1024 : 8192;
+  const int64_t gcap = M::ncf ? 1024 : 8192;
   if (grid > gcap) grid = gcap;
   if (runs) grid = runs_grid;
   phase_begin(c, 2, s);
@@ -3593,47 +2875,30 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
                          c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
                          c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-    else if (use_mfma) {
+    else {
       if constexpr (mfma_ok) {
-        auto kern = k_score_mf_mfma<M, false, kMfmaCPI, 1>;
-        if (rel_idx && influence) {
-          kern = k_score_mf_mfma<M, true, kMfmaCPI, 0>;
-          if (mfma_cpi == 1) kern = mfma_setup == 2 ? k_score_mf_mfma<M, true, 1, 2> : mfma_setup == 1 ? k_score_mf_mfma<M, true, 1, 1> : k_score_mf_mfma<M, true, 1, 0>;
-          else if (mfma_setup == 1) kern = k_score_mf_mfma<M, true, kMfmaCPI, 1>;
-          else if (mfma_setup == 2) kern = k_score_mf_mfma<M, true, kMfmaCPI, 2>;
-        }
-        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
-                           c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
-                           c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                           c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-      }
-    } else if constexpr (one_pass)
-      hipLaunchKernelGGL(k_score_grouped_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
-                         c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
-                         c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                         c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-    else
-      hipLaunchKernelGGL(k_score_grouped<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
-                         c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
-                         c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
-                         c->cand_val.as<double>());
-  } else {
-    // MF k <= 16: item runs (k_score_mf_runs); FIA_MF_SCORE=old: the per-query chunk kernel
-    if constexpr (!M::ncf) {
-      if constexpr (M::K <= 16) {
-        if (runs) {
-          FIA_HIP_TRY(launch_score_mf_runs(M::K, grid, s, A, Q, c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
-                                           c->slices.as<int32_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                                           c->cand_pos.as<int32_t>(), c->cand_val.as<double>()));
+        if (use_mfma) {
+          auto kern = rel_idx && influence ? k_score_mf_mfma<M, true> : k_score_mf_mfma<M, false>;
+          hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                             c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                             c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                             c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+          FIA_HIP_TRY(hipGetLastError());
           phase_end(c, 2, s);
           goto topk;
         }
       }
-      hipLaunchKernelGGL(k_score_mf<M>, dim3((unsigned)grid),
-                         dim3(kScoreThreads), 0, s, A, Q, c->coff.as<int64_t>(), c->cdesc.as<ChunkDesc>(),
-                         c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
-                         c->cand_val.as<double>());
+      hipLaunchKernelGGL(k_score_grouped_mf<M>, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, A, nE,
+                         c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                         c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                         c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
     }
+  } else {
+    // MF k <= 16: item runs
+    if constexpr (runs)
+      FIA_HIP_TRY(launch_score_mf_runs(M::K, grid, s, A, Q, c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
+                                       c->slices.as<int32_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>()));
   }
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 2, s);

@@ -5,11 +5,10 @@
 
 #include "kern.h"
 
-#ifndef FIA_RUNS_WAVES
-#define FIA_RUNS_WAVES 3
-#endif
 
 namespace fia {
+
+constexpr int kRunsWaves = 3;   // waves per SIMD the register budget is sized for
 namespace {
 
 // The wave's best (key, position, value) under the strict (key desc, position asc) order,
@@ -131,7 +130,7 @@ __device__ __forceinline__ void wave_top1_fast(double& a, int& p, double& v) {
 
 // KM: 0 = no top-K, 1 = top-1, 2 = top-K for K_top > 1
 template <class M, int KM>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FIA_RUNS_WAVES))) void k_score_mf_runs(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))) void k_score_mf_runs(
     RunArgs A, int64_t Q, const ChunkDesc* __restrict__ cdesc, const int64_t* __restrict__ qbase,
     const int32_t* __restrict__ slices, const double* __restrict__ rec, int32_t* __restrict__ rel_idx,
     double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {

@@ -130,7 +130,8 @@ class Context(object):
         self._check(self.lib.fia_prepare(self.h, _stream()), "fia_prepare")
 
     def prepare_for(self, qu, qi):
-        """Hessian caches for only the users/items of these queries (large-k models)."""
+        """Hessian caches for only the users/items of these queries (fia_prepare_for, every
+        model: small k marks the entities on the device, large k builds a compact cache)."""
         self._check(self.lib.fia_prepare_for(self.h, qu.numel(), _ptr(qu), _ptr(qi), _stream()), "fia_prepare_for")
 
     def num_params(self):

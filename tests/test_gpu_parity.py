@@ -406,44 +406,6 @@ def test_mf_entity_shared_topk_paths(k, K, tmp_path):
         check_topk(res["topk_pos"][q], res["influence"][b:e], o["influence"], K)
 
 
-def test_mf_item_run_schedule_variant():
-    """The opt-in MF k <= 16 item-run schedule (FIA_MF_SCORE=run: k_score_mf_run + the
-    per-list-position residual pass) passes the same MF golden, duplicate-row, full-ml-1m-ex
-    and scan-window checks.  The schedule is read once per process, so the checks run in a
-    child pytest with the knob set."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FIA_MF_SCORE="run", FIA_RUN_QB="4")
-    sel = ("small_golden and mf or duplicate_rows or ml1m_rq1_golden and MF or ml1m_all_queries "
-           "or ml1m_deterministic or many_queries_scan_windows and MF-16 or every_built_size and MF-8 "
-           "or every_built_size and MF-16")
-    r = subprocess.run([sys.executable, "-m", "pytest", os.path.join(root, "tests", "test_gpu_parity.py"), "-m", "gpu",
-                        "-q", "-x", "-p", "no:cacheprovider", "-k", sel], env=env, cwd=root, capture_output=True,
-                       text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout and "deselected" in r.stdout
-
-
-@pytest.mark.parametrize("mode", ["col", "tile", "cols"])
-def test_ncf_side_solve_variants(mode):
-    """The A/B side solves (FIA_SOLVE=col: k_solve_col, tile: k_solve_tile, cols: the
-    one-column-per-lane k_solve) read the NCF k=16 Gram caches in their row-pair layout (gidx)
-    and pass the NCF golden and every-built-size oracle checks.  The knob is read once per
-    process, so the checks run in a child pytest with it set."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, FIA_SOLVE=mode)
-    sel = ("small_golden and ncf or ml1m_rq1_golden and NCF or yelp_ncf_sample or every_built_size and NCF-16 "
-           "or every_built_size and NCF-8")
-    r = subprocess.run([sys.executable, "-m", "pytest", os.path.join(root, "tests", "test_gpu_parity.py"), "-m", "gpu",
-                        "-q", "-x", "-p", "no:cacheprovider", "-k", sel], env=env, cwd=root, capture_output=True,
-                       text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout and "deselected" in r.stdout
-
-
 @pytest.mark.parametrize("name", ["small_mf_k16.npz", "small_ncf_k16.npz"])
 def test_cached_inverse_hvp_force_refresh_false(name, tmp_path):
     """get_influence_on_test_loss(force_refresh=False) with the reference's cached
