@@ -32,6 +32,46 @@ void phase_end(fia_ctx* c, int phase, hipStream_t s) {
   (void)hipEventRecord(c->events.ev[phase].back().second, s);
 }
 
+// The stream a small-k Gram pass runs on: the context's aux stream, made to wait for
+// everything queued on `s` so far; `s` itself while `s` is being captured into a graph (a
+// fork there would have to be joined inside the same capture) or when aux is unavailable.
+hipStream_t prepare_stream(fia_ctx* c, hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return s;
+  if (!c->aux) {
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) { c->aux = nullptr; return s; }
+    if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->prep_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->l1_ev, hipEventDisableTiming) != hipSuccess)
+      return s;
+  }
+  if (hipEventRecord(c->fork_ev, s) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess) return s;
+  return c->aux;
+}
+
+// after the pass was queued on ps: the point later consumers on the caller's stream join
+hipError_t prepare_record(fia_ctx* c, hipStream_t ps, hipStream_t s) {
+  if (ps == s) return hipSuccess;
+  FIA_HIP_TRY(hipEventRecord(c->prep_ev, ps));
+  c->prep_pending = true;
+  return hipSuccess;
+}
+
+hipError_t join_prepare(fia_ctx* c, hipStream_t s) {
+  c->l1_pending = false;           // recorded before prep_ev on the same stream
+  if (!c->prep_pending) return hipSuccess;
+  FIA_HIP_TRY(hipStreamWaitEvent(s, c->prep_ev, 0));
+  c->prep_pending = false;
+  return hipSuccess;
+}
+
+hipError_t join_l1(fia_ctx* c, hipStream_t s) {
+  if (!c->l1_pending) return join_prepare(c, s);
+  FIA_HIP_TRY(hipStreamWaitEvent(s, c->l1_ev, 0));
+  c->l1_pending = false;
+  return hipSuccess;
+}
+
 }  // namespace fia
 
 namespace {
@@ -78,6 +118,7 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // regrow during a capture).
 hipError_t enter_stream(fia_ctx* c, hipStream_t s) {
   if (c->has_stream && c->stream != s) {
+    if (hipError_t e = fia::join_prepare(c, c->stream); e != hipSuccess) return e;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(c->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
       hipError_t e = hipStreamSynchronize(c->stream);
@@ -137,6 +178,10 @@ int fia_destroy(fia_ctx* c) {
                            &c->cpllist, &c->lscr, &c->mark, &c->d1tab};
     for (auto* b : bufs) b->release(nullptr);
     (void)hipDeviceSynchronize();   // the stream-ordered frees complete before the context goes
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->l1_ev) (void)hipEventDestroy(c->l1_ev);
+    if (c->prep_ev) (void)hipEventDestroy(c->prep_ev);
     for (auto& v : c->events.ev)
       for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto e : c->events.pool) (void)hipEventDestroy(e);
@@ -191,6 +236,7 @@ int fia_build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* 
       return fail(c, FIA_ERR_INVALID, "num_users/num_items differ from the registered params");
     DeviceGuard g(c->device);
     if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_build_index");
+    if (hipError_t es = fia::join_prepare(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_build_index");
     std::string why;
     hipError_t e = fia::build_index(c, N, U, I, user, item, rating, as_stream(stream), why);
     c->prepared = false;
@@ -210,10 +256,14 @@ int fia_prepare(fia_ctx* c, void* stream) {
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
     if (hipError_t es = enter_stream(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare");
+    if (hipError_t es = fia::join_prepare(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare");
     bool unsup = false;
-    fia::phase_begin(c, 0, s);
-    hipError_t e = fia::prepare_model(c, s, unsup);
-    fia::phase_end(c, 0, s);
+    // small k: the Gram pass on the aux stream (the large-k prepare synchronises inside)
+    const hipStream_t ps = fia::big_supported(c->p.model, c->p.k) ? s : fia::prepare_stream(c, s);
+    fia::phase_begin(c, 0, ps);
+    hipError_t e = fia::prepare_model(c, ps, unsup);
+    fia::phase_end(c, 0, ps);
+    if (e == hipSuccess) e = fia::prepare_record(c, ps, s);
     c->prepared = false;
     if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
     if (e == hipErrorOutOfMemory) return fail(c, FIA_ERR_NOMEM, "device memory exhausted by the Hessian caches");
@@ -233,15 +283,23 @@ int fia_prepare_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
     if (hipError_t es = enter_stream(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare_for");
+    // the marks below are read by a still-queued Gram pass
+    if (hipError_t es = fia::join_prepare(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare_for");
     bool unsup = false;
     hipError_t e;
-    fia::phase_begin(c, 0, s);
     if (fia::big_supported(c->p.model, c->p.k)) {
+      fia::phase_begin(c, 0, s);
       e = fia::prepare_big(c, Q, qu, qi, s);
+      fia::phase_end(c, 0, s);
     } else {
-      e = fia::prepare_model_for(c, Q, qu, qi, s, unsup);   // small k: marked entities only, no sync
+      // small k: entities marked on s (no sync), their Gram caches on the aux stream
+      fia::phase_begin(c, 0, s);
+      e = fia::prepare_model_for(c, Q, qu, qi, s, s, unsup, true);
+      const hipStream_t ps = e == hipSuccess ? fia::prepare_stream(c, s) : s;
+      if (e == hipSuccess && !unsup) e = fia::prepare_model_for(c, Q, qu, qi, s, ps, unsup, false);
+      fia::phase_end(c, 0, ps);
+      if (e == hipSuccess) e = fia::prepare_record(c, ps, s);
     }
-    fia::phase_end(c, 0, s);
     c->prepared = false;
     if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
     if (e == hipErrorOutOfMemory) return fail(c, FIA_ERR_NOMEM, "device memory exhausted by the Hessian caches");
@@ -318,6 +376,9 @@ static int query_batch_common(fia_ctx* c, int64_t Q, const int32_t* qu, const in
     if (Q == 0) return FIA_OK;
     DeviceGuard g(c->device);
     if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
+    // (small k joins the pending Gram pass right before its solve, after the query scans)
+    if (fia::big_supported(c->p.model, c->p.k))
+      if (hipError_t es = fia::join_prepare(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
     // chunk descriptors / candidate slots: at most 2 per query + one per kRunChunk ratings
     const int64_t max_chunks = 2 * Q + total_rel / fia::kRunChunk + 1;
     bool unsup = false;

@@ -227,6 +227,16 @@ struct fia_ctx {
   // on the calling stream only)
   hipStream_t stream = nullptr;
   bool has_stream = false;
+  // small-k fia_prepare runs its Gram pass on `aux`, forked from the calling stream, so the
+  // query-side scans of the next calls overlap it; the first consumer of the caches (the
+  // solve of fia_query_batch, or any call that rewrites what the pass reads) joins `prep`
+  hipStream_t aux = nullptr;
+  hipEvent_t fork_ev = nullptr, prep_ev = nullptr;
+  bool prep_pending = false;
+  // NCF: the per-entity layer-1 rows (the first kernels of the pass), which the query-side MLP
+  // prologue reads before the Gram caches are done
+  hipEvent_t l1_ev = nullptr;
+  bool l1_pending = false;
   unsigned profiling = 0;   // bit p: record phase p (fia_set_profiling)
   fia::PhaseEvents events;
 };
@@ -256,8 +266,14 @@ hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
 // model kernels: return hipErrorInvalidValue-style codes, or set `unsupported`
 hipError_t prepare_model(fia_ctx* c, hipStream_t s, bool& unsupported);
 // small k: caches of the queries' users and items only (fia_prepare_for); marks in c->mark
-hipError_t prepare_model_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s,
-                             bool& unsupported);
+hipStream_t prepare_stream(fia_ctx* c, hipStream_t s);
+hipError_t prepare_record(fia_ctx* c, hipStream_t ps, hipStream_t s);
+hipError_t join_prepare(fia_ctx* c, hipStream_t s);
+hipError_t join_l1(fia_ctx* c, hipStream_t s);
+// fia_prepare_for, small k, in two calls: mark_only marks the queries' entities on s; then
+// their Gram caches on ps
+hipError_t prepare_model_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s, hipStream_t ps,
+                             bool& unsupported, bool mark_only);
 hipError_t check_cover_small(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int32_t* flag,
                              hipStream_t s);
 hipError_t query_model(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,

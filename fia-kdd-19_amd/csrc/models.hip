@@ -2259,6 +2259,19 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
           val[r] = fma((R[3] - y) * al[r], R[2], be[r]);
         }
       }
+      // rotate each row by its misalignment dl: lane cn takes element (cn - dl) & 15 -- of
+      // this tile (cn >= dl) or, already rotated, of the previous tile (cn < dl) -- so each
+      // store is one aligned 16-element segment (whole lines: no line written twice).  All
+      // twelve cross-lane reads are issued before the first store: one LDS wait per tile
+      // instead of one per row
+      double rv[4];
+      int32_t rw[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int srcl = ((cn - dl[r]) & 15) + 16 * kk;
+        rv[r] = __shfl(val[r], srcl);
+        rw[r] = __shfl(w, srcl);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const bool ok = pv && qv[r];
@@ -2267,20 +2280,17 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2
         bk[r] = take ? key : bk[r];
         bp[r] = take ? p : bp[r];
         bv[r] = take ? val[r] : bv[r];
-        // rotate the row by its misalignment dl: lane cn takes element (cn - dl) & 15 -- of
-        // this tile (cn >= dl) or, already rotated, of the previous tile (cn < dl) -- so each
-        // store is one aligned 16-element segment (whole lines: no line written twice)
-        const int srcl = ((cn - dl[r]) & 15) + 16 * kk;
-        const double rv = __shfl(val[r], srcl);
-        const int32_t rw = __shfl(w, srcl);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
         const bool cur = cn >= dl[r];
         const int idx = 16 * t + cn - dl[r];          // element of the run this lane stores
         if (qv[r] && (cur ? idx < len : t > 0)) {
-          if (FULL || influence) st_out(cur ? rv : prv[r], outp[r] + 16 * t + cn);
-          if (FULL || rel_idx) st_out(cur ? rw : prw[r], relp[r] + 16 * t + cn);
+          if (FULL || influence) st_out(cur ? rv[r] : prv[r], outp[r] + 16 * t + cn);
+          if (FULL || rel_idx) st_out(cur ? rw[r] : prw[r], relp[r] + 16 * t + cn);
         }
-        prv[r] = rv;
-        prw[r] = rw;
+        prv[r] = rv[r];
+        prw[r] = rw[r];
       }
       if (t % TPC == TPC - 1 || t == ntl - 1) emit(t / TPC);
     };
@@ -2708,6 +2718,10 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
         FIA_HIP_TRY(hipGetLastError());
       }
     }
+    if (s == c->aux && c->l1_ev) {       // on the aux stream: the query prologue may start here
+      FIA_HIP_TRY(hipEventRecord(c->l1_ev, s));
+      c->l1_pending = true;
+    }
   }
   constexpr int GSP = (GS + 1) & ~1;
   // Gram slice length: short slices for parallelism, long enough that the partial Grams
@@ -2810,6 +2824,28 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
   phase_end(c, 4, s);
   phase_begin(c, 1, s);
+  // the query-side work that needs no Gram cache, ahead of the join with a pending prepare:
+  // NCF k = 16 the per-query MLP prologue (after the layer-1 rows), k <= 16 the d1 table
+  if constexpr (pair_layout<M>()) {
+    if (Q > 0 && !x_in) {
+      FIA_HIP_TRY(join_l1(c, s));
+      FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
+      hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(256), 0, s, A, Q,
+                         c->qwork.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+  }
+  if constexpr (mask_path<M>()) {
+    if (Q > 0) {
+      constexpr int NT = (1 << (M::K / 2)) * M::K;
+      FIA_HIP_TRY(c->d1tab.reserve(sizeof(double) * NT, s));
+      hipLaunchKernelGGL(k_ncf_d1_table<M>, dim3((unsigned)((NT + 255) / 256)), dim3(256), 0, s, c->p.t[6], c->p.t[8],
+                         c->d1tab.as<double>());
+      FIA_HIP_TRY(hipGetLastError());
+      A.d1tab = c->d1tab.as<double>();
+    }
+  }
+  FIA_HIP_TRY(join_prepare(c, s));     // the Gram caches (and NCF rows) of a pending fia_prepare
   if (x_in && Q > 0) {
     // a given inverse HVP: records straight from it, no solve (fia_query_batch_x)
     const int64_t g1 = Q < 8192 ? Q : 8192;
@@ -2823,9 +2859,6 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                          c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else if constexpr (pair_layout<M>()) {
-      FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(Q * qpro_stride<M>() + 1), s));
-      hipLaunchKernelGGL(k_ncf_query_pro<M>, dim3((unsigned)((Q + 63) / 64)), dim3(256), 0, s, A, Q,
-                         c->qwork.as<double>());
       hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
                          (const double*)c->qwork.as<double>(), c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else if constexpr (use_col_solve<M>()) {
@@ -2853,11 +2886,6 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     if (Q > 0) {       // the records' MLP block -> y = W1_side^T x_mlp for k_score_ncf
       hipLaunchKernelGGL(k_ncf_rec_y<M>, dim3((unsigned)((2 * Q + 255) / 256)), dim3(256), 0, s, Q, c->p.t[4],
                          c->rec.as<double>());
-      constexpr int NT = (1 << (M::K / 2)) * M::K;
-      FIA_HIP_TRY(c->d1tab.reserve(sizeof(double) * NT, s));
-      hipLaunchKernelGGL(k_ncf_d1_table<M>, dim3((unsigned)((NT + 255) / 256)), dim3(256), 0, s, c->p.t[6], c->p.t[8],
-                         c->d1tab.as<double>());
-      A.d1tab = c->d1tab.as<double>();
     }
   }
   FIA_HIP_TRY(hipGetLastError());
@@ -2988,23 +3016,26 @@ __global__ void k_check_mark(int64_t Q, const int32_t* __restrict__ qu, const in
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
-hipError_t prepare_model_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s,
-                             bool& unsupported) {
+hipError_t prepare_model_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s, hipStream_t ps,
+                             bool& unsupported, bool mark_only) {
   unsupported = false;
   const int64_t U = c->p.U, I = c->p.I;
-  FIA_HIP_TRY(c->mark.reserve((size_t)(U + I), s));
-  FIA_HIP_TRY(hipMemsetAsync(c->mark.ptr, 0, (size_t)(U + I), s));
-  if (Q > 0) {
-    const int64_t gq = (Q + 255) / 256;
-    hipLaunchKernelGGL(k_mark_small, dim3((unsigned)(gq < 4096 ? gq : 4096)), dim3(256), 0, s, Q, qu, qi, U, I,
-                       c->mark.as<uint8_t>());
-    FIA_HIP_TRY(hipGetLastError());
+  if (mark_only) {
+    FIA_HIP_TRY(c->mark.reserve((size_t)(U + I), s));
+    FIA_HIP_TRY(hipMemsetAsync(c->mark.ptr, 0, (size_t)(U + I), s));
+    if (Q > 0) {
+      const int64_t gq = (Q + 255) / 256;
+      hipLaunchKernelGGL(k_mark_small, dim3((unsigned)(gq < 4096 ? gq : 4096)), dim3(256), 0, s, Q, qu, qi, U, I,
+                         c->mark.as<uint8_t>());
+      FIA_HIP_TRY(hipGetLastError());
+    }
+    c->subset = false;
+    c->small_subset = false;
+    return hipSuccess;
   }
-  c->subset = false;
-  c->small_subset = false;
 #define X(m, kk, T)                                                     \
   if (c->p.model == m && c->p.k == kk) {                                \
-    FIA_HIP_TRY(prepare_impl<T>(c, s, c->mark.as<uint8_t>()));          \
+    FIA_HIP_TRY(prepare_impl<T>(c, ps, c->mark.as<uint8_t>()));         \
     c->small_subset = true;                                             \
     return hipSuccess;                                                  \
   }

@@ -68,8 +68,9 @@ __device__ __forceinline__ void wave_top1(double& a, int& p, double& v) {
 // chunk is work only for the first query of a run of equal test items, <= kRunQB queries; a
 // user-side chunk has a run of one).  A batch in item-major order -- the natural way to answer
 // a test set -- shares each popular item's list across its queries without any group build;
-// any order stays correct (runs of one).  Persistent waves, descriptors strided over them.
-// Per descriptor, one wave (2 ratings per lane):
+// any order stays correct (runs of one).  The descriptor list is cut into slices of about
+// equal cost (build_chunks: kRunUserCost per user-side descriptor, 2 + nq per item-side one),
+// one one-wave workgroup per slice.  Per descriptor, one wave (2 ratings per lane):
 //   * the list entries (other id, rating, train row) were loaded during the previous
 //     descriptor; the chunk's other-side rows + biases are gathered ONCE (random 64-B rows
 //     from the L2-resident tables) and converted to f64 once;
