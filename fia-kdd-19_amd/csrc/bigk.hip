@@ -1776,13 +1776,12 @@ hipError_t query_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_
                      c->xb.as<double>(), c->rec.as<double>(), x_out);
   FIA_HIP_TRY(hipGetLastError());
   phase_end(c, 1, s);
-  phase_begin(c, 2, s);
-  hipLaunchKernelGGL(k_big_score_mfma<M>, dim3(grid_cap(max_chunks, 8192)), dim3(256), 0, s, A, c->p.U + c->p.I,
-                     c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
-                     c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K, c->cand_pos.as<int32_t>(),
-                     c->cand_val.as<double>());
+  const PhaseSpan span = phase_span(c, 2);
+  hipExtLaunchKernelGGL(k_big_score_mfma<M>, dim3(grid_cap(max_chunks, 8192)), dim3(256), 0, s, span.a, span.b, 0, A,
+                        c->p.U + c->p.I, c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                        c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                        c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
   FIA_HIP_TRY(hipGetLastError());
-  phase_end(c, 2, s);
   if (K > 0) {
     phase_begin(c, 3, s);
     FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, NPASS, topk_pos, topk_idx, topk_val, s, max_chunks));

@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -33,6 +34,8 @@ struct ChunkDesc {
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
+constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
+constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
 
 // Device buffer with grow-on-demand capacity (never shrinks), allocated from the
@@ -217,7 +220,8 @@ struct fia_ctx {
   int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0}, n_bcache[2] = {0, 0};
   uint64_t bitems_version = ~0ull;
   int bitems_k = 0;
-  fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta
+  fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta (MF k in {32, 64}:
+                          //   the MFMA scoring kernel's store sink)
   fia::DevBuf xb;         // double [Q * 2 NPs] per-query solution (padded side blocks)
   fia::DevBuf syslist;    // int32 [1 + 2Q] {count, 2q + side ...} uncoupled side systems
   fia::DevBuf cpllist;    // int32 [1 + Q]  {count, q ...} coupled full systems
@@ -296,11 +300,22 @@ hipError_t query_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi
                      int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
                      const double* x_in = nullptr);
 // MF k <= 16 item-run scoring (score_mf.hip); QueryArgs is in kern.h
+// a one-kernel phase (scoring) timed by its own dispatch: the event pair goes to
+// hipExtLaunchKernelGGL, which stamps the kernel's start and end from the dispatch packet
+// (two marker packets around it idled the GPU ~5 us each); both null when not profiling
+struct PhaseSpan {
+  hipEvent_t a = nullptr, b = nullptr;
+};
 struct QueryArgs;
+hipError_t launch_score_mf_mfma_t(int k, bool full, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t nE,
+                                  const int64_t* wstart, const int32_t* witems, const int64_t* gstart,
+                                  const int32_t* gq, const int64_t* qbase, const double* rec, int32_t* rel_idx,
+                                  double* influence, int K, int32_t* cand_pos, double* cand_val, double* sink,
+                                  PhaseSpan ps);
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t Q,
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
-                                double* cand_val);
+                                double* cand_val, PhaseSpan ps);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
@@ -309,6 +324,7 @@ hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int
 // phase event helpers (no-ops unless profiling)
 void phase_begin(fia_ctx* c, int phase, hipStream_t s);
 void phase_end(fia_ctx* c, int phase, hipStream_t s);
+PhaseSpan phase_span(fia_ctx* c, int phase);
 
 }  // namespace fia
 

@@ -234,7 +234,10 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     if (lane == 0) {
       s_prefix = excl;
       s_prefix2 = excl2;
-      if (MODE == 1 && tile == 0 && zero_word) zero_word[0] = 0;   // solve's coupled-query counter
+      if (MODE == 1 && tile == 0 && zero_word) {   // the solve's coupled-query counters
+        zero_word[0] = 0;
+        zero_word[1] = 0;
+      }
     }
   }
   __syncthreads();

@@ -165,10 +165,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
       rw[r] = rr[li];
     }
   };
+  // the record and output-base lines of a descriptor's queries, touched by vector loads one
+  // descriptor ahead: a record is read by few descriptors, so its words' scalar loads would
+  // miss L2 (MALL latency) once per query
+  auto touch = [&](int64_t c) -> float {
+    const ChunkDesc dn = cdesc[c];
+    const int nqn = dn.side >> 8;
+    const char* rb = reinterpret_cast<const char*>(rec + (int64_t)dn.q * M::R);
+    const int nl = (nqn * M::R * 8 + 63) / 64 + 1;          // 64-B lines of the run's records
+    const char* qb = reinterpret_cast<const char*>(qbase + 4 * (int64_t)dn.q);
+    const int nb = (nqn * 32 + 63) / 64 + 1;
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int l = r * 64 + lane;
+      t += *reinterpret_cast<const float*>(rb + 64 * (l < nl ? l : 0));
+    }
+    t += *reinterpret_cast<const float*>(qb + 64 * (lane < nb ? lane : 0));
+    return t;
+  };
   int32_t o[RT], row[RT];
   float y[RT];
   fetch(ch, o, y, row);
   int64_t nx = ch + 1 < cend ? ch + 1 : -1;      // the next descriptor (-1: none)
+  float sink = touch(ch);
   while (true) {
     const ChunkDesc d = cdesc[ch];
     const int sd = d.side & 0xff, nq = d.side >> 8;
@@ -194,6 +214,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
     int32_t no[RT], nrow[RT];
     float ny[RT];
     fetch(more ? nx : ch, no, ny, nrow);
+    const float touched = touch(more ? nx : ch);
 
     // rows to f64 (once per descriptor) and 2 e_j, from the run head's record: the entity's
     // own embedding a and b_e + g (scalar loads)
@@ -338,12 +359,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
         }
       }
     } while (++j < nq);
+    sink += touched;     // consumed after this descriptor's stores: no early wait
     if (!more) break;
     ch = nx;
     nx = ch + 1 < cend ? ch + 1 : -1;
 #pragma unroll
     for (int r = 0; r < RT; ++r) { o[r] = no[r]; y[r] = ny[r]; row[r] = nrow[r]; }
   }
+  // keeps the touches (Q >= 1 whenever the kernel runs: never stores)
+  if (Q < 0) cand_pos[lane] = (int32_t)__float_as_uint(sink);
 }
 
 }  // namespace
@@ -351,7 +375,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& QA, int64_t Q,
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
-                                double* cand_val) {
+                                double* cand_val, PhaseSpan ps) {
   RunArgs A{};
   for (int sd = 0; sd < 2; ++sd) {
     A.other[sd] = QA.other[sd];
@@ -361,7 +385,8 @@ hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryA
     A.bias_other[sd] = QA.t[sd == 0 ? 3 : 2];
   }
 #define FIA_RUNS_LAUNCH(KK, KM)                                                                                      \
-  hipLaunchKernelGGL((k_score_mf_runs<MFm<KK>, KM>), dim3((unsigned)grid), dim3(64), 0, s, A, Q, cdesc,           \
+  hipExtLaunchKernelGGL((k_score_mf_runs<MFm<KK>, KM>), dim3((unsigned)grid), dim3(64), 0, s, ps.a, ps.b, 0, A, Q, \
+                        cdesc,                                                                                    \
                      qbase, slices, rec, rel_idx, influence, K, cand_pos, cand_val)
   const int km = K <= 0 ? 0 : K == 1 ? 1 : 2;
   if (k == 16) {

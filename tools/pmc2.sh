@@ -9,7 +9,7 @@ mkdir -p gpurun_out/pmc2
 i=0
 for p in "$@"; do
   i=$((i+1))
-  timeout -k 10 400 rocprofv3 --pmc $p --kernel-include-regex "$re" -d "gpurun_out/pmc2/${tag}_$i" -o run \
+  timeout -k 10 100 rocprofv3 --pmc $p --kernel-include-regex "$re" -d "gpurun_out/pmc2/${tag}_$i" -o run \
       --output-format csv -- python3 bench.py --no-cpu-baseline $bargs > "gpurun_out/pmc2/${tag}_$i.log" 2>&1
   rc=$?
   echo "pmc pass $i ($p) exit $rc"
