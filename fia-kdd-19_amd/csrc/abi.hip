@@ -48,12 +48,6 @@ PhaseSpan phase_span(fia_ctx* c, int phase) {
 // everything queued on `s` so far; `s` itself while `s` is being captured into a graph (a
 // fork there would have to be joined inside the same capture) or when aux is unavailable.
 hipStream_t prepare_stream(fia_ctx* c, hipStream_t s) {
-  // MF k <= 16: the query scans the fork would overlap (~20 us at ml-1m-ex) barely exceed the
-  // cross-queue wait of the join (~10 us on MI355X) and run slower beside the Gram pass:
-  // measured 0.182 vs 0.175 ms per ml-1m-ex step, so those models stay on one stream
-#ifndef FIA_FORK_ALL
-  if (c->p.model == FIA_MODEL_MF && c->p.k <= 16) return s;
-#endif
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return s;
   if (!c->aux) {

@@ -220,8 +220,7 @@ struct fia_ctx {
   int64_t n_bitems[2] = {0, 0}, n_bcomb[2] = {0, 0}, n_bslots[2] = {0, 0}, n_bcache[2] = {0, 0};
   uint64_t bitems_version = ~0ull;
   int bitems_k = 0;
-  fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta (MF k in {32, 64}:
-                          //   the MFMA scoring kernel's store sink)
+  fia::DevBuf qwork;      // double [Q * QW] per-query n, dup terms, r-hat, v, theta
   fia::DevBuf xb;         // double [Q * 2 NPs] per-query solution (padded side blocks)
   fia::DevBuf syslist;    // int32 [1 + 2Q] {count, 2q + side ...} uncoupled side systems
   fia::DevBuf cpllist;    // int32 [1 + Q]  {count, q ...} coupled full systems
@@ -307,11 +306,6 @@ struct PhaseSpan {
   hipEvent_t a = nullptr, b = nullptr;
 };
 struct QueryArgs;
-hipError_t launch_score_mf_mfma_t(int k, bool full, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t nE,
-                                  const int64_t* wstart, const int32_t* witems, const int64_t* gstart,
-                                  const int32_t* gq, const int64_t* qbase, const double* rec, int32_t* rel_idx,
-                                  double* influence, int K, int32_t* cand_pos, double* cand_val, double* sink,
-                                  PhaseSpan ps);
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t Q,
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,

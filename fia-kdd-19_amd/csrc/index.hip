@@ -234,10 +234,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
     if (lane == 0) {
       s_prefix = excl;
       s_prefix2 = excl2;
-      if (MODE == 1 && tile == 0 && zero_word) {   // the solve's coupled-query counters
-        zero_word[0] = 0;
-        zero_word[1] = 0;
-      }
+      if (MODE == 1 && tile == 0 && zero_word) zero_word[0] = 0;   // solve's coupled-query counter
     }
   }
   __syncthreads();
@@ -700,11 +697,6 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
   return hipGetLastError();
 }
 
-// queries per item-run block (A/B knob FIA_RUN_QB, 1 = no sharing)
-static int run_qb() {
-  static const int v = getenv("FIA_RUN_QB") ? atoi(getenv("FIA_RUN_QB")) : kRunQB;
-  return v < 1 ? 1 : v > kRunQB ? kRunQB : v;
-}
 
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word, bool runs,
@@ -722,7 +714,7 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
   }
   return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
                               offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s,
-                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? run_qb() : 0, rq ? kRunChunk : kChunk, lsh,
+                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? kRunQB : 0, rq ? kRunChunk : kChunk, lsh,
                               rq ? c->slices.as<int32_t>() : nullptr);
 }
 

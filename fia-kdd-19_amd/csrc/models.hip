@@ -225,12 +225,10 @@ __device__ void solve_epilogue(const QueryArgs& A, int64_t q, int32_t u, int32_t
 
 // One wave per query, the full D x D packed LDL^T: the queries whose test pair is a train row
 // (its Hessian couples the user and item blocks; the side-system solves list them in qlist
-// {count, done counter, q_0, q_1, ...}).  Work items w0, w0 + wstride, ...; ATOMIC: the list is
-// read with device-scope atomic loads (a caller that saw the writers finish by an atomic
-// counter, not by a kernel boundary).
-template <class M, bool ATOMIC>
-__device__ void solve_full(QueryArgs A, int64_t Q, double* __restrict__ rec, double* __restrict__ x_out,
-                           const int32_t* __restrict__ qlist, int64_t w0, int64_t wstride) {
+// {count, q_0, q_1, ...}).
+template <class M>
+__global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
+                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist) {
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2;
   __shared__ double H[D * (D + 1) / 2];
   __shared__ double v[D], g[D], th[D], dd[D], ww[D];
@@ -244,14 +242,10 @@ __device__ void solve_full(QueryArgs A, int64_t Q, double* __restrict__ rec, dou
     for (int t = threadIdx.x; t < 2 * K * K; t += blockDim.x) sW1[t] = (double)A.t[4][t];
     for (int t = threadIdx.x; t < K; t += blockDim.x) sb1[t] = (double)A.t[5][t];
   }
-  auto listed = [&](int64_t j) -> int32_t {
-    if constexpr (ATOMIC) return __hip_atomic_load(qlist + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return qlist[j];
-  };
-  const int64_t nwork = listed(0);
-  for (int64_t wk = w0; wk < nwork; wk += wstride) {
+  const int64_t nwork = qlist[0];
+  for (int64_t wk = blockIdx.x; wk < nwork; wk += gridDim.x) {
   __syncthreads();
-  const int64_t q = listed(2 + wk);
+  const int64_t q = qlist[1 + wk];
   const int lane = threadIdx.x;
   const int32_t u = A.qu[q], i = A.qi[q];
   double* R = rec + q * M::R;
@@ -317,12 +311,6 @@ __device__ void solve_full(QueryArgs A, int64_t Q, double* __restrict__ rec, dou
 
   solve_epilogue<M>(A, q, u, i, n, rhat_ui, th, g, v, w, R, x_out);
   }   // work loop
-}
-
-template <class M>
-__global__ __launch_bounds__(kSolveThreads, (M::Ds <= 33 ? 2 : 1)) void k_solve(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                                         double* __restrict__ x_out, const int32_t* __restrict__ qlist) {
-  solve_full<M, false>(A, Q, rec, x_out, qlist, blockIdx.x, gridDim.x);
 }
 
 // Scoring records from a GIVEN inverse HVP (fia_query_batch_x: the reference's cached
@@ -613,7 +601,7 @@ __device__ void tile_factor(int g, int c, d4_t (&U)[NT * (NT + 1) / 2], d4_t (&R
 // NCF weights staged once per workgroup.  Every global load of a query (ids of the next
 // query, list pointers, the pair-set probe, both Gram blocks, MF: the right-hand side) is
 // issued before its first dependent use, so a query waits on about two memory latencies.
-// Queries whose test pair is a train row (coupled blocks) go to `coupled` {count, done, q...} for
+// Queries whose test pair is a train row (coupled blocks) go to `coupled` {count, q...} for
 // the full-D k_solve<M, false>.
 template <class M>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(tile_waves<M>()))) void k_solve_tile(
@@ -690,7 +678,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(tile_waves<
     if (cdup > 0.0) {
       if (threadIdx.x == 0) {
         const int slot = atomicAdd(coupled_out, 1);
-        coupled_out[2 + slot] = (int32_t)q;
+        coupled_out[1 + slot] = (int32_t)q;
       }
       continue;
     }
@@ -1001,7 +989,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(col_waves<M>
         if (sd == 0 && t == 0) rec[q * M::R] = NAN;
       } else if (q < Q && sd == 0 && t == 0) {      // coupled: the full-D solve finishes it
         const int slot = atomicAdd(coupled_out, 1);
-        coupled_out[2 + slot] = (int32_t)q;
+        coupled_out[1 + slot] = (int32_t)q;
       }
     }
   }
@@ -1288,7 +1276,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRowsWaves))
     if (sd == 0 && t == 0) rec[q * M::R] = NAN;
   } else if (qok && sd == 0 && t == 0) {          // coupled: the full-D solve finishes it
     const int slot = atomicAdd(coupled_out, 1);
-    coupled_out[2 + slot] = (int32_t)q;
+    coupled_out[1 + slot] = (int32_t)q;
   }
 }
 
@@ -1300,8 +1288,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRowsWaves))
 // `coupled` list and solved afterwards by k_solve (one wave, full D).
 // ------------------------------------------------------------------------------------
 template <class M>
-__device__ __forceinline__ void solve_tps_body(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                               double* __restrict__ x_out, int32_t* __restrict__ coupled) {
+__global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double* __restrict__ rec,
+                                                  double* __restrict__ x_out, int32_t* __restrict__ coupled) {
   static_assert(!M::ncf, "thread-per-system solve is the MF path");
   constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   const int lane = threadIdx.x;
@@ -1335,7 +1323,7 @@ __device__ __forceinline__ void solve_tps_body(QueryArgs A, int64_t Q, double* _
     A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
   if (active && n > 0 && cdup > 0.0 && side == 0) {
     const int slot = atomicAdd(coupled, 1);
-    coupled[2 + slot] = (int32_t)q;
+    coupled[1 + slot] = (int32_t)q;
   }
   if (active && n == 0) {
     if (x_out)
@@ -1426,22 +1414,6 @@ __device__ __forceinline__ void solve_tps_body(QueryArgs A, int64_t Q, double* _
     for (int a = 0; a < Ds; ++a) x_out[q * D + M::ref_index(side * Ds + a)] = x[a];
 }
 
-// k_solve_tps with the coupled queries folded in: the workgroup that finishes last (an atomic
-// count of finished workgroups, coupled[1], reset by it for the next launch) solves the listed
-// coupled queries full-D -- usually none, which saves the separate launch (~4 us at ml-1m-ex)
-template <class M>
-__global__ __launch_bounds__(64) void k_solve_tps_all(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                                      double* __restrict__ x_out, int32_t* __restrict__ coupled) {
-  solve_tps_body<M>(A, Q, rec, x_out, coupled);
-  __shared__ int last;
-  __threadfence();                        // this workgroup's list entries before its count
-  if (threadIdx.x == 0) last = atomicAdd(coupled + 1, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (threadIdx.x == 0) coupled[1] = 0;
-  solve_full<M, true>(A, Q, rec, x_out, coupled, 0, 1);
-}
 
 // ------------------------------------------------------------------------------------
 // MF Gram on the f64 matrix cores: one wave per entity, 4 list rows per
@@ -2727,8 +2699,9 @@ constexpr bool solve_covered() {
   return use_tps<M>() || pair_layout<M>() || use_col_solve<M>() || use_tile_solve<M>();
 }
 
-// MF k <= 16 item runs: slice cost target (descriptor cost units per one-wave slice)
-constexpr int kRunLambda = 32;
+// MF k <= 16 item runs: slice cost target (descriptor cost units per one-wave slice; ml-1m-ex
+// same-box A/B, scoring us: 8 -> 69.4, 16 -> 68.6, 32 -> 73.5, 64 -> 78.6)
+constexpr int kRunLambda = 16;
 
 template <class M>
 hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
@@ -2837,15 +2810,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int64_t nE = c->idx.U + c->idx.I;
   // every (entity chunk, query block) item covers >= 1 per-query chunk
   const int64_t max_items = max_chunks;
-  // the queries whose test pair is a train row are listed in `coupled` {count, done, q...} by
-  // the solve and finished full-D; the chunk scan zeroes both counters
-  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 2), s));
+  // the queries whose test pair is a train row are listed in `coupled` {count, q...} by the
+  // solve and finished full-D; the chunk scan zeroes the count
+  FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
   phase_begin(c, 4, s);
   // MF k <= 16 item runs: one wave per equal-cost slice of the descriptor list (descriptor
   // costs vary ~10x: a static stride over descriptors left waves idle for half the kernel);
   // the slice count is known on the device only -- the grid is its bound (total cost <=
   // kRunUserCost per descriptor slot), the surplus waves exit at once
-  static const int64_t lam = getenv("FIA_RUNS_LAMBDA") ? atoll(getenv("FIA_RUNS_LAMBDA")) : kRunLambda;  // TEMP A/B
+  constexpr int64_t lam = kRunLambda;
   const int64_t runs_grid = (kRunUserCost * (max_chunks + 1)) / lam + 2;
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
@@ -2883,7 +2856,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
   if (Q > 0 && !x_in) {
     if constexpr (use_tps<M>()) {
-      hipLaunchKernelGGL(k_solve_tps_all<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
+      hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                          c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else if constexpr (pair_layout<M>()) {
       hipLaunchKernelGGL(k_solve_rows<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q,
@@ -2903,14 +2876,13 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     }
     FIA_HIP_TRY(hipGetLastError());
     // usually no coupled query: a small grid that exits (a full grid for the large full-D
-    // systems of k >= 32, should many test pairs be train rows); k_solve_tps_all solves them
-    // itself
-    if constexpr (!use_tps<M>()) {
-      const int64_t gc = M::K <= 16 ? 64 : 256;
-      const int64_t g2 = Q < gc ? Q : gc;
-      hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
-                         (const int32_t*)c->coupled.as<int32_t>());
-    }
+    // systems of k >= 32, should many test pairs be train rows).  (Folding this into the last
+    // workgroup of k_solve_tps -- an atomic finish count -- made that kernel 14 us slower at
+    // ml-1m-ex: the full-D solve's LDS and registers in every workgroup)
+    const int64_t gc = M::K <= 16 ? 64 : 256;
+    const int64_t g2 = Q < gc ? Q : gc;
+    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
+                       (const int32_t*)c->coupled.as<int32_t>());
   }
   if constexpr (mask_path<M>()) {
     if (Q > 0) {       // the records' MLP block -> y = W1_side^T x_mlp for k_score_ncf
@@ -2936,12 +2908,12 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     else {
       if constexpr (mfma_ok) {
         if (use_mfma) {
-          FIA_HIP_TRY(c->qwork.reserve(sizeof(double) * (size_t)(grid * (kScoreThreads / 64) * 128), s));   // the sink
-          FIA_HIP_TRY(launch_score_mf_mfma_t(M::K, rel_idx && influence, grid, s, A, nE, c->wstart.as<int64_t>(),
-                                             c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
-                                             c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                                             c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), c->qwork.as<double>(),
-                                             span));
+          auto kern = rel_idx && influence ? k_score_mf_mfma<M, true> : k_score_mf_mfma<M, false>;
+          hipExtLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, span.a, span.b, 0, A, nE,
+                                c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
+                                c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence,
+                                K, c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
+          FIA_HIP_TRY(hipGetLastError());
           goto topk;
         }
       }

@@ -165,30 +165,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
       rw[r] = rr[li];
     }
   };
-  // the record and output-base lines of a descriptor's queries, touched by vector loads one
-  // descriptor ahead: a record is read by few descriptors, so its words' scalar loads would
-  // miss L2 (MALL latency) once per query
-  auto touch = [&](int64_t c) -> float {
-    const ChunkDesc dn = cdesc[c];
-    const int nqn = dn.side >> 8;
-    const char* rb = reinterpret_cast<const char*>(rec + (int64_t)dn.q * M::R);
-    const int nl = (nqn * M::R * 8 + 63) / 64 + 1;          // 64-B lines of the run's records
-    const char* qb = reinterpret_cast<const char*>(qbase + 4 * (int64_t)dn.q);
-    const int nb = (nqn * 32 + 63) / 64 + 1;
-    float t = 0.f;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int l = r * 64 + lane;
-      t += *reinterpret_cast<const float*>(rb + 64 * (l < nl ? l : 0));
-    }
-    t += *reinterpret_cast<const float*>(qb + 64 * (lane < nb ? lane : 0));
-    return t;
-  };
   int32_t o[RT], row[RT];
   float y[RT];
   fetch(ch, o, y, row);
   int64_t nx = ch + 1 < cend ? ch + 1 : -1;      // the next descriptor (-1: none)
-  float sink = touch(ch);
   while (true) {
     const ChunkDesc d = cdesc[ch];
     const int sd = d.side & 0xff, nq = d.side >> 8;
@@ -214,7 +194,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
     int32_t no[RT], nrow[RT];
     float ny[RT];
     fetch(more ? nx : ch, no, ny, nrow);
-    const float touched = touch(more ? nx : ch);
 
     // rows to f64 (once per descriptor) and 2 e_j, from the run head's record: the entity's
     // own embedding a and b_e + g (scalar loads)
@@ -359,15 +338,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
         }
       }
     } while (++j < nq);
-    sink += touched;     // consumed after this descriptor's stores: no early wait
     if (!more) break;
     ch = nx;
     nx = ch + 1 < cend ? ch + 1 : -1;
 #pragma unroll
     for (int r = 0; r < RT; ++r) { o[r] = no[r]; y[r] = ny[r]; row[r] = nrow[r]; }
   }
-  // keeps the touches (Q >= 1 whenever the kernel runs: never stores)
-  if (Q < 0) cand_pos[lane] = (int32_t)__float_as_uint(sink);
 }
 
 }  // namespace
