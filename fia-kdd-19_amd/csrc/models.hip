@@ -1512,7 +1512,20 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
       id_n = id_nn;
     }
   } else {
-    for (int t0 = 0; t0 < len; t0 += 4 * SUB) {
+    // k <= 16 (a work item is <= 256 rows = 4 batches): every batch's row ids loaded up front
+    // (one latency instead of one per batch), the gathers batch by batch
+    constexpr int NB = 4;
+    int32_t idb[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) idb[b] = ids_at(4 * SUB * b);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (4 * SUB * b >= len) break;
+      double val[SUB][NT];
+      gather(idb[b], val);
+      accumulate(val);
+    }
+    for (int t0 = 4 * SUB * NB; t0 < len; t0 += 4 * SUB) {      // (longer work items)
       double val[SUB][NT];
       gather(ids_at(t0), val);
       accumulate(val);
