@@ -48,6 +48,10 @@ PhaseSpan phase_span(fia_ctx* c, int phase) {
 // everything queued on `s` so far; `s` itself while `s` is being captured into a graph (a
 // fork there would have to be joined inside the same capture) or when aux is unavailable.
 hipStream_t prepare_stream(fia_ctx* c, hipStream_t s) {
+  // MF k <= 16: the query scans the fork would overlap (~20 us at ml-1m-ex) barely exceed the
+  // cross-queue wait of the join (~10 us on MI355X), and they run slower beside the Gram pass:
+  // same-box A/B 0.172-0.173 ms per ml-1m-ex step on one stream vs 0.176-0.182 forked
+  if (c->p.model == FIA_MODEL_MF && c->p.k <= 16) return s;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return s;
   if (!c->aux) {
