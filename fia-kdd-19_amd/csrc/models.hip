@@ -2415,16 +2415,39 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_ncf(
   const int64_t n_items = wstart[nE];
   const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
   const int64_t N = A.N;
-  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
-    const int32_t g = witems[3 * wi], cidx = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
+  // work-item headers two stages ahead (scalar loads): the {entity, chunk, block} words of item
+  // i + 2 and the list / group bounds of item i + 1 are in flight while item i is scored (most
+  // yelp-ex items are short lists: the header chain was two of an item's ~four latencies)
+  struct Words { int32_t g, cidx, qblk; };
+  struct Bounds { int64_t p0, p1, s0, s1; };
+  auto words = [&](int64_t w) {
+    const int64_t wc = w < n_items ? w : n_items - 1;
+    return Words{witems[3 * wc], witems[3 * wc + 1], witems[3 * wc + 2]};
+  };
+  auto bounds = [&](const Words& w) {
+    const int sd = w.g >= A.U ? 1 : 0;
+    const int32_t e = sd ? (int32_t)(w.g - A.U) : w.g;
+    return Bounds{A.ptr[sd][e], A.ptr[sd][e + 1], gstart[w.g], gstart[w.g + 1]};
+  };
+  int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave;
+  if (wi >= n_items) return;
+  Words w_cur = words(wi);
+  Bounds b_cur = bounds(w_cur);
+  Words w_nxt = words(wi + stride);
+  for (; wi < n_items; wi += stride) {
+    const Words w_n = w_nxt;
+    const Bounds b_n = bounds(w_n);
+    w_nxt = words(wi + 2 * stride);
+    const int32_t g = w_cur.g, cidx = w_cur.cidx, qblk = w_cur.qblk;
     const int sd = g >= A.U ? 1 : 0;
-    const int32_t e = sd ? (int32_t)(g - A.U) : g;
-    const int64_t lb = A.ptr[sd][e] + (int64_t)cidx * kChunk;
-    const int64_t rem = A.ptr[sd][e + 1] - lb;
+    const int64_t lb = b_cur.p0 + (int64_t)cidx * kChunk;
+    const int64_t rem = b_cur.p1 - lb;
     const int len = rem < kChunk ? (int)rem : kChunk;
-    const int64_t gb = gstart[g] + (int64_t)qblk * QB;
-    const int64_t gn = gstart[g + 1] - gb;
+    const int64_t gb = b_cur.s0 + (int64_t)qblk * QB;
+    const int64_t gn = b_cur.s1 - gb;
     const int nq = gn < QB ? (int)gn : QB;
+    w_cur = w_n;
+    b_cur = b_n;
 
     const int32_t* __restrict__ oth = A.other[sd] + lb;
     const float* __restrict__ rat = A.rating[sd] + lb;
