@@ -13,8 +13,8 @@ re-launches this script under torch.distributed.run with N ranks before anything
 touches the GPU; under torchrun (the driver) WORLD_SIZE/RANK/LOCAL_RANK are read
 from the environment.  Scaling (`--scaling`; every config defaults to strong):
   * strong: the config's fixed query set is split into N contiguous ranges balanced
-    by the related-set sizes n_q (influence.sharding.shard_ranges); every rank
-    answers its range.  On one GPU, `--shard-of S --shard-index r` answers range r
+    by n_q + query_cost (the related-set size plus a per-query fixed cost, CONFIGS;
+    influence.sharding.shard_ranges); every rank answers its range.  On one GPU, `--shard-of S --shard-index r` answers range r
     of an S-way split (one rank's share of an S-GPU job);
   * weak (opt-in): every rank answers one full-size query set -- rank 0 the
     workload's own pairs, rank r > 0 the same users and item multiset re-paired by
@@ -50,17 +50,21 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FP64_PEAK_TFS = 78.6       # MI355X dense FP64 (vector and matrix; tools/mb_f64.hip measures ~70)
 
+# query_cost: a query's fixed work (its solve, chunk lists and share of the Gram pass) in units
+# of one related rating's scoring time, for the strong-scaling split (n_q + query_cost per
+# query); from the round-4 per-phase timings: e.g. 20M MF k=64 61 ns per
+# query over 6.0 ps per scored rating
 CONFIGS = {
     "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m",
-                    scaling="strong"),
+                    scaling="strong", query_cost=560),
     "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp",
-                     scaling="strong"),
+                     scaling="strong", query_cost=210),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
-                     k=64, data="20m", scaling="strong"),
+                     k=64, data="20m", scaling="strong", query_cost=10100),
     "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "
-                      "blocks per query)", model="MF", k=256, data="20m", scaling="strong"),
+                      "blocks per query)", model="MF", k=256, data="20m", scaling="strong", query_cost=150000),
     "20m-ncf256": dict(workload="NCF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 512^2 "
-                       "blocks per query)", model="NCF", k=256, data="20m", scaling="strong"),
+                       "blocks per query)", model="NCF", k=256, data="20m", scaling="strong", query_cost=310000),
 }
 
 
@@ -455,7 +459,7 @@ def main():
     # this rank's queries and every rank's count
     if scaling == "strong" and (world > 1 or args.shard_of > 1):
         S = world if world > 1 else args.shard_of
-        rs = shard_ranges(n_q, S)
+        rs = shard_ranges(n_q + cfg["query_cost"], S)
         all_sizes = [b - a for a, b in rs][:world] if world > 1 else [rs[0][1] - rs[0][0]]
         if world == 1 and not 0 <= args.shard_index < S:
             raise SystemExit("bench: --shard-index %d outside 0 .. %d" % (args.shard_index, S - 1))

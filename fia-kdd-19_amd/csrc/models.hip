@@ -2858,10 +2858,9 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int64_t runs_grid = (kRunUserCost * (max_chunks + 1)) / lam + 2;
   FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
-  phase_end(c, 4, s);
-  phase_begin(c, 1, s);
   // the query-side work that needs no Gram cache, ahead of the join with a pending prepare:
   // NCF k = 16 the per-query MLP prologue (after the layer-1 rows), k <= 16 the d1 table
+  // (timed with the chunk lists: the solve phase starts after the join)
   if constexpr (pair_layout<M>()) {
     if (Q > 0 && !x_in) {
       FIA_HIP_TRY(join_l1(c, s));
@@ -2881,7 +2880,9 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       A.d1tab = c->d1tab.as<double>();
     }
   }
+  phase_end(c, 4, s);
   FIA_HIP_TRY(join_prepare(c, s));     // the Gram caches (and NCF rows) of a pending fia_prepare
+  phase_begin(c, 1, s);
   if (x_in && Q > 0) {
     // a given inverse HVP: records straight from it, no solve (fia_query_batch_x)
     const int64_t g1 = Q < 8192 ? Q : 8192;

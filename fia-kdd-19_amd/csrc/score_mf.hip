@@ -223,20 +223,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
     // compiler's preheader flush (which would wait for the next descriptor's list loads)
 #pragma unroll
     for (int r = 0; r < RT; ++r) asm volatile("" : "+v"(o[r]), "+v"(row[r]));
-    int j = 0;
-    do {
-      // query q0 + j: its words by scalar loads
-      const int32_t qj = q0 + j;
+    // the words of query q0 + j by scalar loads; the next query's are issued once this
+    // query's are consumed (same registers) and land while its top-1 reduction runs
+    struct Words {
+      double x[K], inv_n, cq, xsb, dup;
+      int64_t ou, oi, slot;
+    };
+    auto words = [&](int32_t qj) {
+      Words w;
       const double* __restrict__ Rj = rec + (int64_t)qj * M::R;
       const double* __restrict__ Sj = Rj + 4 + sd * M::SB;
       const int64_t* __restrict__ qb = qbase + 4 * (int64_t)qj;
+#pragma unroll
+      for (int c = 0; c < K; ++c) w.x[c] = Sj[K + c];
+      w.inv_n = Rj[0];
+      w.cq = Rj[1];
+      w.xsb = Sj[2 * K + 1];
+      w.dup = Sj[2 * K + 2];
+      w.ou = qb[0];
+      w.oi = qb[1];
+      w.slot = qb[2 + sd];
+      return w;
+    };
+    Words wj = words(q0);
+    int j = 0;
+    do {
+      const int32_t qj = q0 + j;
+      const double* __restrict__ Rj = rec + (int64_t)qj * M::R;
       // two partial sums per rating (even / odd coordinates): 2 RT independent FMA chains
       double s[RT], s2[RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r) s[r] = s2[r] = 0.0;
 #pragma unroll
       for (int c = 0; c < K; c += 2) {
-        const double xc = Sj[K + c], xd = Sj[K + c + 1];
+        const double xc = wj.x[c], xd = wj.x[c + 1];
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
           s[r] = fma(xc, g[r][c], s[r]);
@@ -245,9 +265,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
       }
 #pragma unroll
       for (int r = 0; r < RT; ++r) s[r] += s2[r];
-      const double inv_nj = Rj[0], cqj = Rj[1], xsbj = Sj[2 * K + 1];
-      const int32_t dupj = (int32_t)Sj[2 * K + 2];
-      const int64_t ou = qb[0], oi = qb[1];
+      const double inv_nj = wj.inv_n, cqj = wj.cq, xsbj = wj.xsb;
+      const int32_t dupj = (int32_t)wj.dup;
+      const int64_t ou = wj.ou, oi = wj.oi;
       const int64_t obj = sd ? oi : ou;
       double infl[RT];
       bool anyd = false;
@@ -283,9 +303,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
           __builtin_amdgcn_raw_buffer_store_b32((unsigned)row[r], rr, idx * 4, 0, kBufNT);
         }
       }
+      const int64_t slot = wj.slot + co / kRunChunk;
+      const int32_t pbj = sd ? (int32_t)(oi - ou) : 0;
+      wj = words(j + 1 < nq ? qj + 1 : qj);
       if constexpr (KM != 0) {
-        const int64_t slot = qb[2 + sd] + co / kRunChunk;
-        const int32_t pbj = sd ? (int32_t)(oi - ou) : 0;
         if constexpr (KM == 1) {
           // the lane's best over its rows (positions ascend with r), then the wave's
           double ba = -2.0, bv = 0.0;
