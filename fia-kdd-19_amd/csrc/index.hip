@@ -151,6 +151,8 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   __shared__ int64_t f_base[MODE == 1 ? kScanTile : 1];
   __shared__ int32_t f_du[MODE == 1 ? kScanTile : 1], f_di[MODE == 1 ? kScanTile : 1];
   __shared__ int32_t f_nq[MODE == 1 ? kScanTile : 1], f_nd[MODE == 1 ? kScanTile : 1];
+  // runs mode: the tile's test items and the kRunQB after it (run heads and lengths from LDS)
+  __shared__ int32_t s_qi[MODE == 1 ? kScanTile + kRunQB : 1];
   const unsigned ntiles = (unsigned)((Q + 1 + kScanTile - 1) / kScanTile);
   if (threadIdx.x == 0) s_tile = (int)atomicAdd(&tctr[0], 1u);
   __syncthreads();
@@ -163,6 +165,18 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
   int64_t s_ub[kScanItems], s_du[kScanItems], s_ib[kScanItems], s_di[kScanItems], s_base[kScanItems];
   int s_nq[kScanItems];
   int64_t tsum = 0, tsum2 = 0;     // tsum2: runs mode, the descriptors' scheduling cost
+  if constexpr (MODE == 1) {
+    static_assert(kScanItems == 1, "one query per thread");
+    if (runs) {
+      const int64_t qa = tile * kScanTile + threadIdx.x;
+      s_qi[threadIdx.x] = qa < Q ? qi[qa] : -1;
+      if (threadIdx.x < kRunQB) {
+        const int64_t qb2 = tile * kScanTile + kScanTile + threadIdx.x;
+        s_qi[kScanTile + threadIdx.x] = qb2 < Q ? qi[qb2] : -1;
+      }
+      __syncthreads();
+    }
+  }
 #pragma unroll
   for (int it = 0; it < kScanItems; ++it) {
     const int64_t q = q0 + it;
@@ -181,13 +195,15 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
           // packed {chunks (candidate slots) << 31 | work descriptors}, chunks of kRunChunk ratings:
           // the item-side chunks are work only for a run head (first query of a run of equal
           // test items, runs cut at multiples of `runs`), which scores them for the whole run
-          const bool head = (q % runs) == 0 || qi[q - 1] != i;
+          const int tt = threadIdx.x;
+          const bool head = (q % runs) == 0 || (tt > 0 ? s_qi[tt - 1] : qi[q - 1]) != i;
           s_nq[it] = 0;
           if (head) {
             int nq = 1;
             const int lim = runs - (int)(q % runs);
+#pragma unroll
             for (int j = 1; j < kRunQB; ++j) {
-              const bool same = j < lim && q + j < Q && qi[q + j] == i;
+              const bool same = j < lim && s_qi[tt + j] == i;      // -1 past the batch
               nq += (same && nq == j) ? 1 : 0;
             }
             s_nq[it] = nq;
