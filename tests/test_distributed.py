@@ -99,3 +99,26 @@ def test_bench_rank_query_sets_are_distinct_and_same_shape():
         assert (q2 != qi).mean() > 0.9
         assert not any(int(u) * I + int(i) in train_key for u, i in zip(qu, q2))
         assert (deg_u[qu] + deg_i[q2]).sum() == (deg_u[qu] + deg_i[qi]).sum()
+
+
+def test_bench_strong_split_with_query_cost():
+    """bench.py strong scaling: every config balances n_q plus its per-query cost; the ranges
+    are contiguous, cover every query once, and --shard-index picks one of them."""
+    import importlib
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    bench = importlib.import_module("bench")
+    rng = np.random.default_rng(5)
+    n_q = rng.integers(20, 3000, 5000)
+    for name, cfg in bench.CONFIGS.items():
+        assert cfg["query_cost"] >= 0, name
+        rs = shard_ranges(n_q + cfg["query_cost"], 8)
+        assert rs[0][0] == 0 and rs[-1][1] == n_q.size
+        assert all(rs[r][1] == rs[r + 1][0] for r in range(7))
+        loads = [(n_q[b:e] + cfg["query_cost"]).sum() for b, e in rs]
+        assert max(loads) <= (n_q + cfg["query_cost"]).sum() / 8 + n_q.max() + cfg["query_cost"]
+    a = bench.parse(["--shard-of", "8", "--shard-index", "5", "--config", "20m-mf64"])
+    assert a.shard_of == 8 and a.shard_index == 5
