@@ -191,7 +191,7 @@ int fia_destroy(fia_ctx* c) {
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
                            &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->gscan,
                            &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,
-                           &c->cpllist, &c->lscr, &c->mark, &c->d1tab};
+                           &c->cpllist, &c->lscr, &c->mark, &c->d1tab, &c->slices, &c->wfrag};
     for (auto* b : bufs) b->release(nullptr);
     (void)hipDeviceSynchronize();   // the stream-ordered frees complete before the context goes
     if (c->aux) (void)hipStreamDestroy(c->aux);

@@ -219,18 +219,58 @@ __global__ void k_l1_big(const float* __restrict__ emb, const float* __restrict_
 // side's positions, so the work is dense.  A row in both kinds of list gets its
 // residual from both passes: the same arithmetic, the same bits.
 constexpr int kRowWaves = 4;
+
+// The MLP weights as f64 MFMA B-operand fragments, built once per prepare (3 k^2 doubles,
+// L2-resident): fragment (t, p) of a product is 64 lanes x 2 doubles, lane (ml, kl)
+// holding the weights of output column 16t + ml at reduction indices 8p + 2kl + {0, 1}
+// (the A operand reads the same two indices as one 16-B LDS word), so every B load of
+// k_ncf_rows is one contiguous 1-KB dwordx4 wave load covering two MFMAs instead of
+// sixteen scattered 16-B row pieces and a convert per MFMA.
+//   [0, HK)        z2 = relu(z1) W2:  W2[kidx][col]      t < H/16, p < K/8
+//   [HK, 2HK)      W2 d2:             W2[col][kidx]      t < K/16, p < H/8
+//   [2HK, 2HK+2K^2) g_mlp, side sd:   W1[sd K + col][kidx] t < K/16, p < K/8
+template <int K>
+__global__ void k_ncf_wfrag(const float* __restrict__ W1, const float* __restrict__ W2, double* __restrict__ wf) {
+  constexpr int H = K / 2;
+  constexpr int64_t n = (int64_t)3 * K * K;
+  for (int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; f < n; f += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(f & 1), lane = (int)((f >> 1) & 63);
+    const int64_t tp = f >> 7;   // fragment index (t, p) within its product
+    const int ml = lane & 15, kl = lane >> 4;
+    double x;
+    if (f < (int64_t)H * K) {
+      const int t = (int)(tp / (K / 8)), p = (int)(tp % (K / 8));
+      x = W2[(8 * p + 2 * kl + i) * H + 16 * t + ml];
+    } else if (f < (int64_t)2 * H * K) {
+      const int64_t q = tp - (int64_t)H * K / 128;
+      const int t = (int)(q / (H / 8)), p = (int)(q % (H / 8));
+      x = W2[(16 * t + ml) * H + 8 * p + 2 * kl + i];
+    } else {
+      const int64_t q = tp - (int64_t)2 * H * K / 128;
+      const int sd = (int)(q / (K / 16 * (K / 8)));
+      const int64_t r = q % (K / 16 * (K / 8));
+      const int t = (int)(r / (K / 8)), p = (int)(r % (K / 8));
+      x = W1[(int64_t)(sd * K + 16 * t + ml) * K + 8 * p + 2 * kl + i];
+    }
+    wf[f] = x;
+  }
+}
+
 template <int K>
 __global__ __launch_bounds__(64 * kRowWaves) void k_ncf_rows(
     int64_t N, int pass, const int32_t* __restrict__ self0, const int32_t* __restrict__ other0,
     const int32_t* __restrict__ row0, const float* __restrict__ rat0, const double* __restrict__ l1u,
     const double* __restrict__ l1i, const float* __restrict__ b1, const float* __restrict__ W2,
     const float* __restrict__ b2, const float* __restrict__ W3, const float* __restrict__ b3,
-    const float* __restrict__ Pg, const float* __restrict__ Qg, const float* __restrict__ W1,
+    const float* __restrict__ Pg, const float* __restrict__ Qg, const double2* __restrict__ wf,
     double* __restrict__ gm0, double* __restrict__ gm1, double* __restrict__ resid,
     const uint8_t* __restrict__ mark, int64_t U) {
   constexpr int H = K / 2, LZ = K + 4, LD2 = H + 4, NW = kRowWaves;
-  __shared__ double Z1[16 * LZ];
-  __shared__ double D2[16 * LD2];
+  __shared__ __attribute__((aligned(16))) double Z1[16 * LZ];
+  __shared__ __attribute__((aligned(16))) double D2[16 * LD2];
+  const double2* __restrict__ Fz2 = wf;
+  const double2* __restrict__ Fd1 = wf + H * K / 2;
+  const double2* __restrict__ Fg = wf + H * K;
   __shared__ double part_mlp[NW][16];
   __shared__ double part_gmf[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -256,10 +296,13 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_ncf_rows(
     double mlp[4] = {0.0, 0.0, 0.0, 0.0};
     for (int t = w; t < H / 16; t += NW) {
       d4_t acc = {0.0, 0.0, 0.0, 0.0};
+      const double2* __restrict__ fb = Fz2 + t * (K / 8) * 64 + lane;
 #pragma unroll 4
-      for (int kk = 0; kk < K; kk += 4) {
-        const double z = Z1[ml * LZ + kk + kl];
-        acc = mfma4(z > 0.0 ? z : 0.0, (double)W2[(kk + kl) * H + 16 * t + ml], acc);
+      for (int p = 0; p < K / 8; ++p) {
+        const double2 z = *reinterpret_cast<const double2*>(Z1 + ml * LZ + 8 * p + 2 * kl);
+        const double2 b = fb[64 * p];
+        acc = mfma4(z.x > 0.0 ? z.x : 0.0, b.x, acc);
+        acc = mfma4(z.y > 0.0 ? z.y : 0.0, b.y, acc);
       }
       const int d = 16 * t + ml;
       const double w3m = (double)W3[d], bb = (double)b2[d];
@@ -293,9 +336,14 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_ncf_rows(
     __syncthreads();
     for (int t = w; t < K / 16; t += NW) {
       d4_t acc = {0.0, 0.0, 0.0, 0.0};
+      const double2* __restrict__ fb = Fd1 + t * (H / 8) * 64 + lane;
 #pragma unroll 4
-      for (int kk = 0; kk < H; kk += 4)
-        acc = mfma4(D2[ml * LD2 + kk + kl], (double)W2[(16 * t + ml) * H + kk + kl], acc);
+      for (int p = 0; p < H / 8; ++p) {
+        const double2 a = *reinterpret_cast<const double2*>(D2 + ml * LD2 + 8 * p + 2 * kl);
+        const double2 b = fb[64 * p];
+        acc = mfma4(a.x, b.x, acc);
+        acc = mfma4(a.y, b.y, acc);
+      }
       const int c = 16 * t + ml;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {           // Z1 becomes D1 (each lane rewrites what it read)
@@ -311,9 +359,14 @@ __global__ __launch_bounds__(64 * kRowWaves) void k_ncf_rows(
       double* __restrict__ gm = sd ? gm1 : gm0;
       for (int t = w; t < K / 16; t += NW) {
         d4_t acc = {0.0, 0.0, 0.0, 0.0};
-        const float* __restrict__ wrow = W1 + (int64_t)(sd * K + 16 * t + ml) * K;
+        const double2* __restrict__ fb = Fg + (sd * (K / 16) + t) * (K / 8) * 64 + lane;
 #pragma unroll 4
-        for (int kk = 0; kk < K; kk += 4) acc = mfma4(Z1[ml * LZ + kk + kl], (double)wrow[kk + kl], acc);
+        for (int p = 0; p < K / 8; ++p) {
+          const double2 a = *reinterpret_cast<const double2*>(Z1 + ml * LZ + 8 * p + 2 * kl);
+          const double2 b = fb[64 * p];
+          acc = mfma4(a.x, b.x, acc);
+          acc = mfma4(a.y, b.y, acc);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = kl + 4 * r;
@@ -344,11 +397,74 @@ constexpr int kBigSlice = 2048;     // ratings per Gram work item
 template <class M>
 struct GramCfg {
   static constexpr int NTL = M::T * (M::T + 1) / 2;
-  static constexpr int MAXPER = 18;                                   // accumulator tiles per wave
+  // accumulator tiles per wave (NCF: fewer, for the prefetched slab registers)
+  static constexpr int MAXPER = M::ncf ? 14 : 18;
   static constexpr int NG = (NTL + kGW * MAXPER - 1) / (kGW * MAXPER);  // tile groups (workgroups per slice)
   static constexpr int TPG = (NTL + NG - 1) / NG;
   static constexpr int PER = (TPG + kGW - 1) / kGW;
   static constexpr int LDG = M::NPs + 16;   // staged g row stride (doubles)
+};
+
+// One staging thread's share of a 16-rating slab (row r of the slab, coordinates
+// pp * PERT + [0, PERT)), loaded into registers one slab ahead and written to LDS as f64.
+// MF: the gathered other-side embedding, then the constant 1 of the bias coordinate;
+// NCF: g_mlp,j of the side (precomputed by k_ncf_rows), then W3g * gmf_other.
+template <class M, bool NCF = M::ncf>
+struct GramStage;
+
+template <class M>
+struct GramStage<M, false> {
+  static constexpr int K = M::K, PERT = K / 32;
+  float4 x[PERT / 4];
+  bool valid;
+  __device__ void fetch(const int32_t* __restrict__ other, const int32_t*, const float* __restrict__ emb,
+                        const double*, int64_t pos, int r, int rem, int pp) {
+    valid = r < rem;
+    const int32_t o = valid ? other[pos + r] : 0;
+    const float4* src = reinterpret_cast<const float4*>(emb + (int64_t)o * K + pp * PERT);
+#pragma unroll
+    for (int c = 0; c < PERT / 4; ++c) x[c] = src[c];
+  }
+  __device__ void put(double* __restrict__ row, const double*, int pp) const {
+#pragma unroll
+    for (int c = 0; c < PERT / 4; ++c) {
+      double* d = row + pp * PERT + 4 * c;
+      d[0] = valid ? (double)x[c].x : 0.0;
+      d[1] = valid ? (double)x[c].y : 0.0;
+      d[2] = valid ? (double)x[c].z : 0.0;
+      d[3] = valid ? (double)x[c].w : 0.0;
+    }
+    if (pp < 16) row[K + pp] = (pp == 0 && valid) ? 1.0 : 0.0;
+  }
+};
+
+template <class M>
+struct GramStage<M, true> {
+  static constexpr int K = M::K, PERT = K / 32;
+  double m[PERT];
+  float g[PERT];
+  bool valid;
+  __device__ void fetch(const int32_t* __restrict__ other, const int32_t* __restrict__ rowid,
+                        const float* __restrict__ emb, const double* __restrict__ gms, int64_t pos, int r, int rem,
+                        int pp) {
+    valid = r < rem;
+    const int32_t o = valid ? other[pos + r] : 0;
+    const int32_t j = valid ? rowid[pos + r] : 0;
+    const double* msrc = gms + (int64_t)j * K + pp * PERT;
+    const float* gsrc = emb + (int64_t)o * K + pp * PERT;
+#pragma unroll
+    for (int c = 0; c < PERT; ++c) {
+      m[c] = msrc[c];
+      g[c] = gsrc[c];
+    }
+  }
+  __device__ void put(double* __restrict__ row, const double* __restrict__ w3g, int pp) const {
+#pragma unroll
+    for (int c = 0; c < PERT; ++c) {
+      row[pp * PERT + c] = valid ? m[c] : 0.0;
+      row[K + pp * PERT + c] = valid ? w3g[pp * PERT + c] * (double)g[c] : 0.0;
+    }
+  }
 };
 
 template <class M>
@@ -360,12 +476,21 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
                                                        const double* __restrict__ gms, const float* __restrict__ W3,
                                                        double* __restrict__ gram, double* __restrict__ part) {
   using C = GramCfg<M>;
-  constexpr int K = M::K, T = M::T, LDG = C::LDG, PER = C::PER;
+  constexpr int T = M::T, LDG = C::LDG, PER = C::PER;
   constexpr int64_t GW = gram_words<M>();
-  __shared__ double Gs[16 * LDG];
+  // two slab buffers: slab n is written to Gs[n & 1] while the waves may still read slab
+  // n - 1 from the other one, so one barrier per slab, and the next slab's global loads
+  // are issued before this slab's MFMAs (they land while the matrix cores run)
+  __shared__ __attribute__((aligned(16))) double Gs[2][16 * LDG];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ml = lane & 15, kl = lane >> 4;
   const int grp = blockIdx.y;
+  const int r = tid >> 5, pp = tid & 31;   // staging: 16 rows x 32 threads
+  __shared__ double w3g[M::ncf ? M::K : 1];   // NCF: W3's GMF weights (f64) for the staging
+  if constexpr (M::ncf)
+    for (int c = tid; c < M::K; c += 64 * kGW) w3g[c] = (double)W3[M::H + c];
+  __syncthreads();
+  GramStage<M> stage;
   const int tend = (grp + 1) * C::TPG < C::NTL ? (grp + 1) * C::TPG : C::NTL;
   int tr_[PER], tc_[PER];
   bool on_[PER];
@@ -378,47 +503,22 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
     tr_[p] = on_[p] ? tr : 0;
     tc_[p] = on_[p] ? idx - tr * (tr + 1) / 2 : 0;
   }
+  int buf = 0;
   for (int64_t it = blockIdx.x; it < n_items; it += gridDim.x) {
     const int32_t e = items[4 * it], start = items[4 * it + 1], len = items[4 * it + 2], dst = items[4 * it + 3];
     const int64_t lb = ptr[e] + start;
     d4_t acc[PER];
 #pragma unroll
     for (int p = 0; p < PER; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
-    for (int t0 = 0; t0 < len; t0 += 16) {
+    stage.fetch(other, rowid, emb_other, gms, lb, r, len, pp);
+    for (int t0 = 0; t0 < len; t0 += 16, buf ^= 1) {
+      double* __restrict__ G = Gs[buf];
+      stage.put(G + r * LDG, w3g, pp);
       __syncthreads();
-      {
-        const int r = tid >> 5, pp = tid & 31;   // 16 rows x 32 threads
-        const bool valid = t0 + r < len;
-        const int32_t o = valid ? other[lb + t0 + r] : 0;
-        if constexpr (!M::ncf) {
-          constexpr int PERT = K / 32;            // floats per thread
-          const float* src = emb_other + (int64_t)o * K + pp * PERT;
-#pragma unroll
-          for (int c = 0; c < PERT; c += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(src + c);
-            double* dst = Gs + r * LDG + pp * PERT + c;
-            dst[0] = valid ? (double)x.x : 0.0;
-            dst[1] = valid ? (double)x.y : 0.0;
-            dst[2] = valid ? (double)x.z : 0.0;
-            dst[3] = valid ? (double)x.w : 0.0;
-          }
-          if (pp < 16) Gs[r * LDG + K + pp] = (pp == 0 && valid) ? 1.0 : 0.0;
-        } else {
-          constexpr int PERT = K / 32;
-          const int32_t j = valid ? rowid[lb + t0 + r] : 0;
-          const double* msrc = gms + (int64_t)j * K + pp * PERT;
-          const float* gsrc = emb_other + (int64_t)o * K + pp * PERT;
-#pragma unroll
-          for (int c = 0; c < PERT; ++c) {
-            Gs[r * LDG + pp * PERT + c] = valid ? msrc[c] : 0.0;
-            Gs[r * LDG + K + pp * PERT + c] = valid ? (double)W3[M::H + pp * PERT + c] * (double)gsrc[c] : 0.0;
-          }
-        }
-      }
-      __syncthreads();
+      if (t0 + 16 < len) stage.fetch(other, rowid, emb_other, gms, lb + t0 + 16, r, len - t0 - 16, pp);
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
-        const double* gr = Gs + (4 * s4 + kl) * LDG + ml;
+        const double* gr = G + (4 * s4 + kl) * LDG + ml;
 #pragma unroll
         for (int p = 0; p < PER; ++p)
           if (on_[p]) acc[p] = mfma4(gr[16 * tr_[p]], gr[16 * tc_[p]], acc[p]);
@@ -435,13 +535,19 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
   }
 }
 
+// partial Grams of a long list summed in slot order; blockIdx.y splits the GW words so a
+// handful of long lists still spreads over every CU
+constexpr int kCombSplit = 64;
 __global__ void k_big_combine(int64_t n_comb, const int32_t* __restrict__ comb, int64_t GW,
                               const double* __restrict__ part, double* __restrict__ gram) {
+  const int64_t per = (GW + kCombSplit - 1) / kCombSplit;
+  const int64_t t0 = (int64_t)blockIdx.y * per, t1 = t0 + per < GW ? t0 + per : GW;
   for (int64_t w = blockIdx.x; w < n_comb; w += gridDim.x) {
     const int32_t gs = comb[4 * w], first = comb[4 * w + 1], ns = comb[4 * w + 2];
-    for (int64_t t = threadIdx.x; t < GW; t += blockDim.x) {
+    const double* __restrict__ src = part + (int64_t)first * GW;
+    for (int64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
       double s = 0.0;
-      for (int k = 0; k < ns; ++k) s += part[(int64_t)(first + k) * GW + t];
+      for (int k = 0; k < ns; ++k) s += src[(int64_t)k * GW + t];
       gram[(int64_t)gs * GW + t] = s;
     }
   }
@@ -1649,13 +1755,17 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
       FIA_HIP_TRY(hipGetLastError());
       FIA_HIP_TRY(c->gm[sd].reserve(sizeof(double) * (size_t)(N * K + 1), s));
     }
+    FIA_HIP_TRY(c->wfrag.reserve(sizeof(double) * (size_t)3 * K * K, s));
+    hipLaunchKernelGGL(k_ncf_wfrag<K>, dim3(3 * K * K / 256), dim3(256), 0, s, c->p.t[4], c->p.t[6],
+                       c->wfrag.as<double>());
+    FIA_HIP_TRY(hipGetLastError());
     for (int pass = qu ? 0 : -1; N > 0 && pass < (qu ? 2 : 0); ++pass) {
       const int sd = pass < 0 ? 0 : pass;
       hipLaunchKernelGGL(k_ncf_rows<K>, dim3(grid_cap((N + 15) / 16, 65536)), dim3(64 * kRowWaves), 0, s, N, pass,
                          c->self[sd].as<int32_t>(), X.side[sd].other.as<int32_t>(), X.side[sd].row.as<int32_t>(),
                          X.side[sd].rating.as<float>(), c->l1[0].as<double>(), c->l1[1].as<double>(), c->p.t[5],
-                         c->p.t[6], c->p.t[7], c->p.t[8], c->p.t[9], c->p.t[2], c->p.t[3], c->p.t[4],
-                         c->gm[0].as<double>(), c->gm[1].as<double>(), c->resid.as<double>(),
+                         c->p.t[6], c->p.t[7], c->p.t[8], c->p.t[9], c->p.t[2], c->p.t[3],
+                         c->wfrag.as<const double2>(), c->gm[0].as<double>(), c->gm[1].as<double>(), c->resid.as<double>(),
                          qu ? c->mark.as<uint8_t>() : (const uint8_t*)nullptr, n_ent[0]);
       FIA_HIP_TRY(hipGetLastError());
     }
@@ -1672,7 +1782,7 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
       FIA_HIP_TRY(hipGetLastError());
     }
     if (c->n_bcomb[sd] > 0) {
-      hipLaunchKernelGGL(k_big_combine, dim3(grid_cap(c->n_bcomb[sd], 65536)), dim3(256), 0, s, c->n_bcomb[sd],
+      hipLaunchKernelGGL(k_big_combine, dim3(grid_cap(c->n_bcomb[sd], 1024), kCombSplit), dim3(256), 0, s, c->n_bcomb[sd],
                          c->bcomb[sd].as<int32_t>(), GW, c->gpart[sd].as<double>(), c->gram[sd].as<double>());
       FIA_HIP_TRY(hipGetLastError());
     }

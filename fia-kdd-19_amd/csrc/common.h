@@ -212,6 +212,7 @@ struct fia_ctx {
                           //   (small-k NCF: [2][N] by list position of each side)
   fia::DevBuf gm[2];      // double [N*k] NCF g_mlp = W1_side . d1_j by train row, per side
                           //   (small-k NCF: [k][N] by list position)
+  fia::DevBuf wfrag;      // large-k NCF: W2 / W1 as f64 MFMA B fragments [3 k^2] (k_ncf_wfrag)
   fia::DevBuf slot[2];    // int32 [n_entity] Gram cache slot (-1 = not cached) after fia_prepare_for
   fia::DevBuf mark;       // uint8 [U + I] entities referenced by the fia_prepare_for queries
   bool subset = false;    // caches cover only the fia_prepare_for entities (large-k models)
