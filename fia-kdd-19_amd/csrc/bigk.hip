@@ -1184,8 +1184,10 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[m][ct][r] = H.at(R0 + 16 * m + kl + 4 * r, c0 + 16 * ct + ml);
-  // panel update: k-steps (4 factored columns each) through a ring of PDT register slots
+      for (int r = 0; r < 4; ++r) acc[m][ct][r] = H.at(R0 + 16 * m + kl + 4 * r, c0 + NT * ml + ct);
+  // panel update: k-steps (4 factored columns each) through a ring of PDT register slots.
+  // Column j of product tile ct is panel column NT j + ct, so a lane's NT B values of a
+  // k-step are consecutive doubles (two 16-B loads instead of four 8-B ones)
   const int nst = active ? c0 >> 2 : 0;
   double ra[PDT][MG], rb[PDT][NT], rd[PDT];
   auto ld = [&](int st, double (&a)[MG], double (&b)[NT], double& d) {
@@ -1194,8 +1196,17 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
     d = dd[k];
 #pragma unroll
     for (int m = 0; m < MG; ++m) a[m] = Lc[R0 + 16 * m + ml];     // rows past LDR: never used (m >= ng)
+    if constexpr (NT % 2 == 0) {
 #pragma unroll
-    for (int ct = 0; ct < NT; ++ct) b[ct] = Lc[c0 + 16 * ct + ml];
+      for (int ct = 0; ct < NT; ct += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(Lc + c0 + NT * ml + ct);
+        b[ct] = v.x;
+        b[ct + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) b[ct] = Lc[c0 + NT * ml + ct];
+    }
   };
 #pragma unroll
   for (int d = 0; d < PDT; ++d)
@@ -1228,7 +1239,7 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
 #pragma unroll
     for (int ct = 0; ct < NT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + 16 * ct + ml] = acc[m][ct][r];
+      for (int r = 0; r < 4; ++r) P[(kl + 4 * r) * LT + NT * ml + ct] = acc[m][ct][r];
     wave_lds_sync();
     double pa[4 * NT];
 #pragma unroll
