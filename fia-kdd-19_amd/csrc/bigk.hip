@@ -402,19 +402,24 @@ struct GramCfg {
   static constexpr int NG = (NTL + kGW * MAXPER - 1) / (kGW * MAXPER);  // tile groups (workgroups per slice)
   static constexpr int TPG = (NTL + NG - 1) / NG;
   static constexpr int PER = (TPG + kGW - 1) / kGW;
-  static constexpr int LDG = M::NPs + 16;   // staged g row stride (doubles)
+  static constexpr int LDT = 18;            // NCF slab: coordinate-major, 16 ratings + 2 pad
+  static constexpr int LDG = M::NPs + 16;   // MF slab: rating-major row stride (doubles)
+  static constexpr int SLAB = M::ncf ? M::NPs * LDT : 16 * LDG;
 };
 
-// One staging thread's share of a 16-rating slab (row r of the slab, coordinates
-// pp * PERT + [0, PERT)), loaded into registers one slab ahead and written to LDS as f64.
-// MF: the gathered other-side embedding, then the constant 1 of the bias coordinate;
-// NCF: g_mlp,j of the side (precomputed by k_ncf_rows), then W3g * gmf_other.
+// One staging thread's share of a 16-rating slab, loaded into registers one slab ahead and
+// written to LDS as f64.  MF: the gathered other-side embedding, then the constant 1 of
+// the bias coordinate, rating-major; NCF: g_mlp,j of the side (precomputed by k_ncf_rows),
+// then W3g * gmf_other, coordinate-major (slab[coord * LDT + rating]: a lane's two ratings
+// of an MFMA pair are one 16-B read, and the 16 lanes of a coordinate write 32 consecutive
+// dwords; config-5 NCF prepare 114.7 -> 107.1 ms, same-box A/B; at MF k = 256 it measured
+// 20.1 vs 19.4 ms and MF keeps the rating-major slab)
 template <class M, bool NCF = M::ncf>
 struct GramStage;
 
 template <class M>
-struct GramStage<M, false> {
-  static constexpr int K = M::K, PERT = K / 32;
+struct GramStage<M, false> {   // rating-major: row r of the slab, coordinates pp * PERT + [0, PERT)
+  static constexpr int K = M::K, PERT = K / 32, LDG = GramCfg<M>::LDG;
   float4 x[PERT / 4];
   bool valid;
   __device__ void fetch(const int32_t* __restrict__ other, const int32_t*, const float* __restrict__ emb,
@@ -425,7 +430,8 @@ struct GramStage<M, false> {
 #pragma unroll
     for (int c = 0; c < PERT / 4; ++c) x[c] = src[c];
   }
-  __device__ void put(double* __restrict__ row, const double*, int pp) const {
+  __device__ void put(double* __restrict__ G, const double*, int r, int pp) const {
+    double* row = G + r * LDG;
 #pragma unroll
     for (int c = 0; c < PERT / 4; ++c) {
       double* d = row + pp * PERT + 4 * c;
@@ -440,29 +446,30 @@ struct GramStage<M, false> {
 
 template <class M>
 struct GramStage<M, true> {
-  static constexpr int K = M::K, PERT = K / 32;
+  static constexpr int K = M::K, PERT = K / 32, LDT = GramCfg<M>::LDT;
   double m[PERT];
   float g[PERT];
   bool valid;
   __device__ void fetch(const int32_t* __restrict__ other, const int32_t* __restrict__ rowid,
                         const float* __restrict__ emb, const double* __restrict__ gms, int64_t pos, int r, int rem,
-                        int pp) {
+                        int q) {
     valid = r < rem;
     const int32_t o = valid ? other[pos + r] : 0;
     const int32_t j = valid ? rowid[pos + r] : 0;
-    const double* msrc = gms + (int64_t)j * K + pp * PERT;
-    const float* gsrc = emb + (int64_t)o * K + pp * PERT;
+    const double* msrc = gms + (int64_t)j * K + q * PERT;
+    const float* gsrc = emb + (int64_t)o * K + q * PERT;
 #pragma unroll
     for (int c = 0; c < PERT; ++c) {
       m[c] = msrc[c];
       g[c] = gsrc[c];
     }
   }
-  __device__ void put(double* __restrict__ row, const double* __restrict__ w3g, int pp) const {
+  __device__ void put(double* __restrict__ G, const double* __restrict__ w3g, int r, int q) const {
+    double* d = G + q * PERT * LDT + r;
 #pragma unroll
     for (int c = 0; c < PERT; ++c) {
-      row[pp * PERT + c] = valid ? m[c] : 0.0;
-      row[K + pp * PERT + c] = valid ? w3g[pp * PERT + c] * (double)g[c] : 0.0;
+      d[c * LDT] = valid ? m[c] : 0.0;
+      d[(K + c) * LDT] = valid ? w3g[q * PERT + c] * (double)g[c] : 0.0;
     }
   }
 };
@@ -476,12 +483,12 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
                                                        const double* __restrict__ gms, const float* __restrict__ W3,
                                                        double* __restrict__ gram, double* __restrict__ part) {
   using C = GramCfg<M>;
-  constexpr int T = M::T, LDG = C::LDG, PER = C::PER;
+  constexpr int T = M::T, LDT = C::LDT, LDG = C::LDG, PER = C::PER;
   constexpr int64_t GW = gram_words<M>();
   // two slab buffers: slab n is written to Gs[n & 1] while the waves may still read slab
   // n - 1 from the other one, so one barrier per slab, and the next slab's global loads
   // are issued before this slab's MFMAs (they land while the matrix cores run)
-  __shared__ __attribute__((aligned(16))) double Gs[2][16 * LDG];
+  __shared__ __attribute__((aligned(16))) double Gs[2][C::SLAB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ml = lane & 15, kl = lane >> 4;
   // NG > 2 (NCF k = 256): XCD-aware order -- block b runs on XCD b % 8 and the NG tile
@@ -492,7 +499,9 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
   constexpr bool XG = C::NG > 2;
   const int grp = XG ? (int)((blockIdx.x >> 3) % C::NG) : (int)blockIdx.y;
   const int64_t n_vb = XG ? ((n_items + 7) / 8) * 8 * C::NG : n_items;
-  const int r = tid >> 5, pp = tid & 31;   // staging: 16 rows x 32 threads
+  // staging thread: rating r, coordinate chunk q (NCF: 16 lanes per coordinate; MF: 32
+  // threads per rating row)
+  const int r = M::ncf ? tid & 15 : tid >> 5, q = M::ncf ? tid >> 4 : tid & 31;
   __shared__ double w3g[M::ncf ? M::K : 1];   // NCF: W3's GMF weights (f64) for the staging
   if constexpr (M::ncf)
     for (int c = tid; c < M::K; c += 64 * kGW) w3g[c] = (double)W3[M::H + c];
@@ -519,18 +528,35 @@ __global__ __launch_bounds__(64 * kGW) void k_big_gram(int sd, int64_t n_items, 
     d4_t acc[PER];
 #pragma unroll
     for (int p = 0; p < PER; ++p) acc[p] = d4_t{0.0, 0.0, 0.0, 0.0};
-    stage.fetch(other, rowid, emb_other, gms, lb, r, len, pp);
+    stage.fetch(other, rowid, emb_other, gms, lb, r, len, q);
     for (int t0 = 0; t0 < len; t0 += 16, buf ^= 1) {
       double* __restrict__ G = Gs[buf];
-      stage.put(G + r * LDG, w3g, pp);
+      stage.put(G, w3g, r, q);
       __syncthreads();
-      if (t0 + 16 < len) stage.fetch(other, rowid, emb_other, gms, lb + t0 + 16, r, len - t0 - 16, pp);
+      if (t0 + 16 < len) stage.fetch(other, rowid, emb_other, gms, lb + t0 + 16, r, len - t0 - 16, q);
+      // MFMA pair h: lane (m, g) supplies ratings 8h + 2g and 8h + 2g + 1 of coordinate
+      // 16 tr + m (A) / 16 tc + m (B), one 16-B read each
+      if constexpr (M::ncf) {
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const double* gr = G + (4 * s4 + kl) * LDG + ml;
+        for (int h = 0; h < 2; ++h) {
+          const double* gc = G + ml * LDT + 8 * h + 2 * kl;
 #pragma unroll
-        for (int p = 0; p < PER; ++p)
-          if (on_[p]) acc[p] = mfma4(gr[16 * tr_[p]], gr[16 * tc_[p]], acc[p]);
+          for (int p = 0; p < PER; ++p)
+            if (on_[p]) {
+              const double2 a = *reinterpret_cast<const double2*>(gc + 16 * LDT * tr_[p]);
+              const double2 b = *reinterpret_cast<const double2*>(gc + 16 * LDT * tc_[p]);
+              acc[p] = mfma4(a.x, b.x, acc[p]);
+              acc[p] = mfma4(a.y, b.y, acc[p]);
+            }
+        }
+      } else {
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const double* gr = G + (4 * s4 + kl) * LDG + ml;
+#pragma unroll
+          for (int p = 0; p < PER; ++p)
+            if (on_[p]) acc[p] = mfma4(gr[16 * tr_[p]], gr[16 * tc_[p]], acc[p]);
+        }
       }
     }
     double* out = dst >= 0 ? gram + (int64_t)dst * GW : part + (int64_t)(-dst - 1) * GW;
