@@ -638,7 +638,11 @@ def main():
             dk = prepare_kernel(cfg)
             flops = prepare_flops(cfg["model"], k, int(tu.size))
             fmodel = "per rating and side: Gram rank-1 update D_s(D_s+1) flops (+ NCF MLP 12 k^2)"
-        dtj = load_traffic(args.traffic_json, args.config, dk)
+        # PMC bytes of the whole phase per launch when recorded (the solve phase is several
+        # kernels, dispatched many times per batch: "<phase>_phase" entries sum them), else the
+        # dominant kernel's own entry
+        dtj = load_traffic(args.traffic_json, args.config, dom + "_phase") or \
+            load_traffic(args.traffic_json, args.config, dk)
         dtraffic = dtj.get("hbm_bytes_per_launch") if dtj else None
         tfs = flops / (ph_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
@@ -647,6 +651,7 @@ def main():
                     "peak_note": "MI355X dense FP64; f64 MFMA and f64 VALU issue to the same DP units (DESIGN.md "
                                  "section 6), so this one peak bounds both",
                     "traffic_gbs": dtraffic / (ph_ms * 1e-3) / 1e9 if dtraffic else None,
+                    "traffic_scope": dtj.get("scope", "kernel " + dk + ", per dispatch") if dtj else None,
                     "score_hbm": score_hbm}
     workload = cfg["workload"]
     if world > 1 and scaling == "weak":
