@@ -55,20 +55,37 @@ hipStream_t prepare_stream(fia_ctx* c, hipStream_t s) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return s;
   if (!c->aux) {
-    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) { c->aux = nullptr; return s; }
-    if (hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->prep_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->l1_ev, hipEventDisableTiming) != hipSuccess)
+    // the stream and its three events all or nothing (a half-made set would fork work that
+    // can never be joined)
+    hipStream_t a = nullptr;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool ok = hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
+    for (int t = 0; t < 3 && ok; ++t) ok = hipEventCreateWithFlags(&ev[t], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+      if (a) (void)hipStreamDestroy(a);
       return s;
+    }
+    c->aux = a;
+    c->fork_ev = ev[0];
+    c->prep_ev = ev[1];
+    c->l1_ev = ev[2];
   }
   if (hipEventRecord(c->fork_ev, s) != hipSuccess || hipStreamWaitEvent(c->aux, c->fork_ev, 0) != hipSuccess) return s;
   return c->aux;
 }
 
-// after the pass was queued on ps: the point later consumers on the caller's stream join
+// after the pass was queued on ps: the point later consumers on the caller's stream join.
+// Called after a failed pass too: the kernels already queued on ps are joined by the next call
+// (or, when even the record fails, waited for here) before any buffer they read can be regrown.
 hipError_t prepare_record(fia_ctx* c, hipStream_t ps, hipStream_t s) {
   if (ps == s) return hipSuccess;
-  FIA_HIP_TRY(hipEventRecord(c->prep_ev, ps));
+  hipError_t e = hipEventRecord(c->prep_ev, ps);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(ps);
+    return e;
+  }
   c->prep_pending = true;
   return hipSuccess;
 }
@@ -169,31 +186,36 @@ int fia_destroy(fia_ctx* c) {
   if (!c) return FIA_OK;
   {
     DeviceGuard g(c->device);
-    (void)hipDeviceSynchronize();
+    // Only the context's own streams are waited for -- never the whole device, which would
+    // also wait for (and, in global capture mode, invalidate a capture on) other streams.
+    // The buffers are freed in order on the context's stream, then that stream is synchronised
+    // so the frees complete before the context goes.  A context that never saw a stream owns
+    // no device buffer.  (Destroying a context while its stream is being captured leaves its
+    // buffers to the pool: they cannot be freed inside someone else's capture.)
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
+    c->prep_pending = c->l1_pending = false;
+    const hipStream_t ds = c->has_stream ? c->stream : nullptr;
+    hipStreamCaptureStatus dcs = hipStreamCaptureStatusNone;
+    const bool can_free = c->has_stream && hipStreamIsCapturing(ds, &dcs) == hipSuccess &&
+                          dcs == hipStreamCaptureStatusNone;
+    if (can_free) (void)hipStreamSynchronize(ds);
+    auto rel = [&](fia::DevBuf& b) {
+      if (can_free) b.release(ds);
+      else { b.ptr = nullptr; b.bytes = 0; }
+    };
     for (int s = 0; s < 2; ++s) {
-      c->idx.side[s].ptr.release(nullptr);
-      c->idx.side[s].row.release(nullptr);
-      c->idx.side[s].other.release(nullptr);
-      c->idx.side[s].rating.release(nullptr);
-      c->gram[s].release(nullptr);
-      c->l1[s].release(nullptr);
-      c->idx.order[s].release(nullptr);
-      c->idx.gitems[s].release(nullptr);
-      c->idx.gcomb[s].release(nullptr);
-      c->gpart[s].release(nullptr);
-      c->self[s].release(nullptr);
-      c->gm[s].release(nullptr);
-      c->slot[s].release(nullptr);
-      c->bitems[s].release(nullptr);
-      c->bcomb[s].release(nullptr);
+      for (fia::DevBuf* b : {&c->idx.side[s].ptr, &c->idx.side[s].row, &c->idx.side[s].other, &c->idx.side[s].rating,
+                             &c->gram[s], &c->l1[s], &c->idx.order[s], &c->idx.gitems[s], &c->idx.gcomb[s],
+                             &c->gpart[s], &c->self[s], &c->gm[s], &c->slot[s], &c->bitems[s], &c->bcomb[s]})
+        rel(*b);
     }
     fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->qscan,
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
                            &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->gscan,
                            &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,
                            &c->cpllist, &c->lscr, &c->mark, &c->d1tab, &c->slices, &c->wfrag};
-    for (auto* b : bufs) b->release(nullptr);
-    (void)hipDeviceSynchronize();   // the stream-ordered frees complete before the context goes
+    for (auto* b : bufs) rel(*b);
+    if (can_free) (void)hipStreamSynchronize(ds);   // the stream-ordered frees complete
     if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->l1_ev) (void)hipEventDestroy(c->l1_ev);
@@ -217,6 +239,13 @@ int fia_set_params(fia_ctx* c, int model, int k, int64_t U, int64_t I, const flo
                    double wd, double damping) {
   if (!c) return FIA_ERR_INVALID;
   FIA_GUARDED(c, {
+    // a small-k Gram pass still queued on the aux stream reads the tables being replaced
+    // (this call has no stream to order behind it: wait for the pass on the host)
+    if (c->prep_pending && c->aux) {
+      DeviceGuard g(c->device);
+      if (hipError_t es = hipStreamSynchronize(c->aux); es != hipSuccess) return hip_fail(c, es, "fia_set_params");
+      c->prep_pending = c->l1_pending = false;
+    }
     if (model != FIA_MODEL_MF && model != FIA_MODEL_NCF) return fail(c, FIA_ERR_INVALID, "unknown model");
     const int need = model == FIA_MODEL_MF ? 5 : 10;
     if (!tables || nptrs != need) return fail(c, FIA_ERR_INVALID, "wrong number of parameter tables");
@@ -279,7 +308,7 @@ int fia_prepare(fia_ctx* c, void* stream) {
     fia::phase_begin(c, 0, ps);
     hipError_t e = fia::prepare_model(c, ps, unsup);
     fia::phase_end(c, 0, ps);
-    if (e == hipSuccess) e = fia::prepare_record(c, ps, s);
+    if (hipError_t er = fia::prepare_record(c, ps, s); e == hipSuccess) e = er;
     c->prepared = false;
     if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");
     if (e == hipErrorOutOfMemory) return fail(c, FIA_ERR_NOMEM, "device memory exhausted by the Hessian caches");
@@ -314,7 +343,7 @@ int fia_prepare_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
       const hipStream_t ps = e == hipSuccess ? fia::prepare_stream(c, s) : s;
       if (e == hipSuccess && !unsup) e = fia::prepare_model_for(c, Q, qu, qi, s, ps, unsup, false);
       fia::phase_end(c, 0, ps);
-      if (e == hipSuccess) e = fia::prepare_record(c, ps, s);
+      if (hipError_t er = fia::prepare_record(c, ps, s); e == hipSuccess) e = er;
     }
     c->prepared = false;
     if (unsup) return fail(c, FIA_ERR_UNSUPPORTED, "model/k not supported");

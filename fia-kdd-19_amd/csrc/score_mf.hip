@@ -139,6 +139,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
   constexpr int K = M::K, RT = kRunChunk / 64, NA = K / 4;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // bytes per rating of the two outputs (0: the caller passed NULL, include/fia.h)
+  const int n_inf = influence ? 8 : 0, n_rel = rel_idx ? 4 : 0;
   // one equal-cost slice of the descriptor list per one-wave workgroup (build_chunks): the
   // hardware dispatcher hands slices to free wave slots, so the work is balanced at slice
   // granularity without atomics; the wave walks its slice's descriptors in order
@@ -290,9 +292,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
       // buffer stores with the chunk's length as the range: lanes past it are dropped by the
       // hardware (no branch around the stores, so every query issues the same number of them
       // and the compiler's vmcnt waits for older loads stay exact); nt policy
+      // (rel_idx / influence NULL -- a top-K-only call: ranges of 0 bytes drop every store; the
+      // bases are formed as integers, never as pointer arithmetic on a null pointer)
       {
-        const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(influence + obj + co, 0, len * 8, kBufWord3);
-        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rel_idx + obj + co, 0, len * 4, kBufWord3);
+        const int64_t ob = obj + co;
+        const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<double*>(reinterpret_cast<uintptr_t>(influence) + (uintptr_t)ob * 8), 0, len * n_inf, kBufWord3);
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<int32_t*>(reinterpret_cast<uintptr_t>(rel_idx) + (uintptr_t)ob * 4), 0, len * n_rel, kBufWord3);
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
           const int idx = r * 64 + lane;

@@ -425,8 +425,10 @@ class GenericNeuralNet(object):
         # Only a flat float64 vector of this model's D values is accepted: the reference
         # itself saves a ragged per-block list (mf:221), which numpy stores as an object
         # array that allow_pickle=False refuses -- such a file, or one of another size, is
-        # treated as absent and the solve runs (pickles are never loaded).
+        # treated as absent and the solve runs (pickles are never loaded), and is left as it is:
+        # the reference never overwrites its cache file when force_refresh is False.
         cached = None
+        unusable = False
         if not force_refresh and os.path.exists(fname):
             try:
                 with np.load(fname, allow_pickle=False) as z:
@@ -435,6 +437,7 @@ class GenericNeuralNet(object):
                     cached = arr.astype(np.float64).reshape(1, -1)
             except (ValueError, KeyError, OSError):
                 cached = None
+            unusable = cached is None
             if self.verbose:
                 print(("Loaded inverse HVP from %s" if cached is not None else
                        "Ignored unusable inverse HVP file %s") % fname)
@@ -445,7 +448,7 @@ class GenericNeuralNet(object):
         x = res["x"][0]
         self.num_params = x.size
         self.inverse_hvp = self._split_theta(x)
-        if self.save_inverse_hvp and cached is None:
+        if self.save_inverse_hvp and cached is None and not unusable:
             np.savez(fname, inverse_hvp=x)
         self.last_timing = rq2_timing(phases, res["influence"].size, time.time() - t0,
                                       log=print if self.verbose else None)

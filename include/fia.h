@@ -61,6 +61,8 @@ int fia_version(void);
 
 /* Create a context bound to HIP device `device`. */
 int fia_create(int device, fia_ctx** out);
+/* Waits for the context's own work (its aux stream and the stream of its last call, not the
+ * whole device), frees its buffers in order on that stream and destroys it. */
 int fia_destroy(fia_ctx* ctx);
 /* Message of the last failing call on ctx ("" if none).  ctx may be NULL. */
 const char* fia_last_error(const fia_ctx* ctx);
@@ -90,7 +92,14 @@ int fia_build_index(fia_ctx* ctx, int64_t n_train, int64_t num_users, int64_t nu
 /* Per-entity Hessian caches for the current params + index: for every user u
  * the Gram sum over R_u of the restricted prediction gradients, likewise for
  * every item (the rank-1 updates of H_t).  Call after set_params/build_index
- * and again whenever the parameter VALUES change. */
+ * and again whenever the parameter VALUES change.
+ * Ordering: the caches are ready for every later call on the context.  For small k
+ * (except MF k <= 16) the pass runs on the context's own stream, forked from `stream`, and
+ * the next fia_* call on the context joins it (the query-side scans of fia_query_batch
+ * overlap it); until then it still READS the parameter tables and the index, so keep the
+ * tables alive and unchanged until the next call on the context -- fia_set_params (which
+ * waits for the pass on the host), fia_build_index, fia_prepare*, fia_query_batch* or
+ * fia_destroy -- rather than only until `stream` is synchronised. */
 int fia_prepare(fia_ctx* ctx, void* stream);
 
 /* Like fia_prepare, but the per-entity caches are built only for the users and items

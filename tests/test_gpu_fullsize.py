@@ -2,8 +2,8 @@
 
   * config 4 -- synthetic 20M ratings, MF k=64: all 276,986 held-out queries in
     fia_query_batch batches (as bench.py runs them), every batch checked on the GPU;
-  * config 5 -- the same ratings, MF k=256 and NCF k=256: one GPU's 1/8 shard of the
-    n_q-balanced split, caches from fia_prepare_for;
+  * config 5 -- the same ratings, MF k=256 and NCF k=256: shards 0, 3 and 7 of the 8-GPU
+    split bench.py runs, caches from fia_prepare_for;
   * config 3 -- yelp-ex NCF k=16: all 51,153 test ratings in one batch.
 
 Size-independent properties, checked for EVERY query with torch on the GPU (the
@@ -191,13 +191,17 @@ def test_config4_mf64_all_queries(data20m):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("shard", [0, 3, 7])
 @pytest.mark.parametrize("model", ["MF", "NCF"])
-def test_config5_k256_shard(data20m, model):
-    """Config 5: k=256 (MF 2 x 257^2, NCF 2 x 512^2 blocks per query) on one GPU's 1/8 shard of
-    the n_q-balanced split, caches from fia_prepare_for; every batch checked; oracle sample
-    with the shard's heaviest item query (NCF: the heaviest below 200k ratings, the CPU
-    oracle's MLP cost) and a train-pair query of the shard's users."""
+def test_config5_k256_shard(data20m, model, shard):
+    """Config 5: k=256 (MF 2 x 257^2, NCF 2 x 512^2 blocks per query) on shards 0, 3 and 7 of
+    the 8-GPU split bench.py runs (n_q + the config's per-query cost, shard_ranges), caches from
+    fia_prepare_for; every batch checked on the GPU; an fp64 oracle sample of >= 16 queries per
+    shard: the shard's heaviest query (no size cap: the heaviest of any shard has ~122 k related
+    ratings), its lightest, 13 random ones and a train-pair query of a shard user (coupled
+    full-D system)."""
     import torch
+    import bench
     from influence.sharding import shard_ranges
     from oracle import fia_oracle as fo
     d = data20m
@@ -209,7 +213,8 @@ def test_config5_k256_shard(data20m, model):
     qu, qi = np.ascontiguousarray(qu[order]), np.ascontiguousarray(qi[order])
     deg_u = np.bincount(d["train"][0], minlength=d["U"])
     deg_i = np.bincount(d["train"][1], minlength=d["I"])
-    b0, b1 = shard_ranges(deg_u[qu] + deg_i[qi], 8)[0]
+    cost = bench.CONFIGS["20m-%s256" % model.lower()]["query_cost"]
+    b0, b1 = shard_ranges(deg_u[qu] + deg_i[qi] + cost, 8)[shard]
     su, si = qu[b0:b1], qi[b0:b1]
     # a train-pair query of a shard user, appended (its item joins the cached set)
     tu, ti, _ = d["train"]
@@ -219,16 +224,17 @@ def test_config5_k256_shard(data20m, model):
     dev = torch.device("cuda", 0)
     ctx.prepare_for(torch.from_numpy(su).to(dev), torch.from_numpy(si).to(dev))
     n = deg_u[su] + deg_i[si]
-    limit = 4_000_000 if model == "MF" else 200_000
-    ok = np.nonzero(n <= limit)[0]
-    heavy = int(ok[np.argmax(n[ok])])
-    rng = np.random.default_rng(1)
-    keep = [heavy, su.size - 1] + [int(q) for q in rng.choice(su.size - 1, 2, replace=False)]
+    heavy, light = int(np.argmax(n[:-1])), int(np.argmin(n[:-1]))
+    rng = np.random.default_rng(1 + shard)
+    rest = np.setdiff1d(np.arange(su.size - 1), [heavy, light])
+    keep = [heavy, light, su.size - 1] + [int(q) for q in rng.choice(rest, 13, replace=False)]
     got, nb, n_q = run_batches(ctx, su, si, 1, GpuChecker(d), keep)
-    assert su.size > 30000 and n_q.sum() > 1e9
+    assert su.size > 12000 and n_q.sum() > 5e8 and len(set(keep)) == 16
     oracle = fo.CsrExact(model, params, k, *d["train"], 1e-3, 1e-6)
     for q in keep:
         compare_oracle(model, k, d, params, int(su[q]), int(si[q]), got[q], oracle)
+    print("config 5 %s shard %d/8: %d queries, %d batches, oracle sample of %d incl. the heaviest (n = %d)"
+          % (model, shard, su.size, nb, len(keep), int(n[heavy])))
     ctx.close()
     torch.cuda.empty_cache()
 

@@ -446,7 +446,7 @@ def test_cached_inverse_hvp_force_refresh_false_large_k(model, k, tmp_path):
     one whose test pair is a train row (the coupled full-D system); the second call matches
     the first to 1e-12 relative, a doubled vector gives exactly doubled influence, and a file
     holding the reference's own ragged per-block list (an object array, refused without
-    pickle) is ignored -- the solve runs instead."""
+    pickle) is ignored -- the solve runs instead, and the file is not overwritten."""
     rng = np.random.default_rng(11)
     U, I, N = 300, 40, 4000
     key = np.sort(rng.choice(U * I, N, replace=False))
@@ -469,5 +469,32 @@ def test_cached_inverse_hvp_force_refresh_false_large_k(model, k, tmp_path):
         ragged = np.empty(4, dtype=object)
         ragged[:] = [x0[:2], x0[2:5], x0[5:6], x0[6:]]
         np.savez(fname, inverse_hvp=ragged)
+        with open(fname, "rb") as fh:
+            ref_bytes = fh.read()
         solved = m.get_influence_on_test_loss([t], np.arange(N), force_refresh=False)
         assert np.array_equal(solved.view(np.int64), first.view(np.int64))
+        with open(fname, "rb") as fh:           # the reference-format file is left as it was
+            assert fh.read() == ref_bytes
+
+
+@pytest.mark.parametrize("k", [8, 16])
+@pytest.mark.parametrize("K", [1, 4])
+def test_mf_small_k_topk_only_no_outputs(k, K, tmp_path):
+    """fia_query_batch with rel_idx = influence = NULL (get_influence_batch(full=False)): the
+    MF k <= 16 item-run kernel drops every per-rating store (zero-length buffer ranges) and the
+    top-K lists equal the full run's."""
+    rng = np.random.default_rng(40 + k)
+    U, I, N = 500, 60, 6000
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = synth.mf_params(U, I, k, 4)
+    qi = np.sort(rng.integers(0, I, 200)).astype(np.int32)      # item runs
+    qu = rng.integers(0, U, 200).astype(np.int32)
+    m = make_model("MF", U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    full = m.get_influence_batch(list(range(qu.size)), K=K)
+    lean = m.get_influence_batch(list(range(qu.size)), K=K, full=False, return_x=False)
+    assert "influence" not in lean and "rel_idx" not in lean
+    for key_ in ("topk_pos", "topk_idx"):
+        assert np.array_equal(lean[key_], full[key_]), key_
+    assert np.array_equal(lean["topk_val"], full["topk_val"], equal_nan=True)
