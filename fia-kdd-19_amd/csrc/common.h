@@ -34,6 +34,9 @@ struct ChunkDesc {
 constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
+constexpr int kGsSub = 16;              // ratings per Gram-stream sub-batch (4 f64 MFMA row-quads)
+constexpr int kGsSlice = 512;           // longest Gram-stream segment (longer lists: partial slices)
+constexpr int kGsTarget = 32;           // sub-batches per Gram-stream wave (at most 64: one per lane)
 constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
 constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
@@ -106,6 +109,15 @@ struct Index {
   std::vector<int64_t> hptr[2];   // host copies of side[s].ptr (Gram work lists)
   std::vector<int32_t> hord[2];   // entities by list length, longest first (host)
   int64_t gchunk = 0;             // list rows per small-k Gram work item of gitems
+  // MF k <= 16 Gram stream (build_gram_stream, k_gram_mf_stream): the lists of both sides cut
+  // into sub-batches of kGsSub ratings, one descriptor each {meta, slot} (meta = valid ratings
+  // | last of its segment << 5 | side << 6 | dummy << 7 | entity << 8), their other-side ids
+  // in stream order (kGsSub per sub-batch, -1 past a list's end), and the first descriptor of
+  // every wave's range (whole lists up to kGsSlice ratings, longer lists in kGsSlice slices
+  // whose partial Grams gscomb sums in slot order)
+  DevBuf gsdesc, gsids, gswave, gscomb[2];
+  int64_t n_gsw = 0, n_gsdesc = 0, n_gscomb[2] = {0, 0}, n_gsslots[2] = {0, 0};
+  uint64_t gs_version = ~0ull;
   uint64_t version = 0;           // bumped by every build_index
   bool valid = false;
 };
@@ -263,6 +275,8 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr,
                         bool runs = false, int slice_cost = 0);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
+// the MF k <= 16 Gram stream of the current index (Index::gs*), rebuilt after build_index
+hipError_t build_gram_stream(fia_ctx* c, hipStream_t s);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_items, int qb, hipStream_t s, int cpi = 1);

@@ -580,6 +580,108 @@ hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s) {
   return hipSuccess;
 }
 
+// the other-side ids of the Gram stream, in stream order: ids[kGsSub d + r] = other[side][pos_d + r]
+// for r < valid_d, else -1
+__global__ void k_gs_ids(int64_t nd, const int2* __restrict__ desc, const int32_t* __restrict__ pos,
+                         const int32_t* __restrict__ other0, const int32_t* __restrict__ other1,
+                         int32_t* __restrict__ ids) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nd * kGsSub;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = t / kGsSub;
+    const int r = (int)(t % kGsSub);
+    const int meta = desc[d].x;
+    const int valid = meta & 31, side = (meta >> 6) & 1;
+    ids[t] = r < valid ? (side ? other1 : other0)[pos[d] + r] : -1;
+  }
+}
+
+hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
+  Index& X = c->idx;
+  if (X.gs_version == X.version && X.gswave.ptr) return hipSuccess;
+  struct Seg {
+    int64_t len;
+    int side;
+    int32_t e, start, slot;
+  };
+  std::vector<Seg> segs;
+  std::vector<int32_t> comb[2];
+  for (int sd = 0; sd < 2; ++sd) {
+    const std::vector<int64_t>& hptr = X.hptr[sd];
+    int32_t slots = 0;
+    for (int32_t e : X.hord[sd]) {
+      const int64_t len = hptr[(size_t)e + 1] - hptr[(size_t)e];
+      if (len <= kGsSlice) {
+        segs.push_back({len, sd, e, 0, -1});
+        continue;
+      }
+      const int64_t nit = (len + kGsSlice - 1) / kGsSlice;
+      comb[sd].insert(comb[sd].end(), {e, slots, (int32_t)nit, 0});
+      for (int64_t t = 0; t < nit; ++t)
+        segs.push_back({std::min<int64_t>(kGsSlice, len - t * kGsSlice), sd, e, (int32_t)(t * kGsSlice), slots++});
+    }
+    X.n_gsslots[sd] = slots;
+  }
+  // longest segments first (both sides merged): the slices of the long lists start early
+  std::stable_sort(segs.begin(), segs.end(), [](const Seg& a, const Seg& b) { return a.len > b.len; });
+  std::vector<int2> desc;
+  std::vector<int32_t> pos, wave{0};
+  int cur = 0;
+  auto close_wave = [&]() {
+    if (cur & 1) {   // an even count per wave (the kernel runs two sub-batches per loop trip)
+      desc.push_back(int2{1 << 7, -1});
+      pos.push_back(0);
+      ++cur;
+    }
+    wave.push_back((int32_t)desc.size());
+    cur = 0;
+  };
+  for (const Seg& g : segs) {
+    const int nsb = g.len == 0 ? 1 : (int)((g.len + kGsSub - 1) / kGsSub);
+    if (cur > 0 && cur + nsb > 62) close_wave();
+    for (int t = 0; t < nsb; ++t) {
+      const int valid = (int)std::min<int64_t>(kGsSub, g.len - (int64_t)t * kGsSub);
+      const int meta = (valid < 0 ? 0 : valid) | (t == nsb - 1 ? 1 << 5 : 0) | (g.side << 6) | (g.e << 8);
+      desc.push_back(int2{meta, g.slot});
+      pos.push_back((int32_t)(X.hptr[g.side][(size_t)g.e] + g.start + (int64_t)t * kGsSub));
+    }
+    cur += nsb;
+    if (cur >= kGsTarget) close_wave();
+  }
+  if (cur > 0) close_wave();
+  const int64_t nd = (int64_t)desc.size();
+  X.n_gsdesc = nd;
+  X.n_gsw = (int64_t)wave.size() - 1;
+  // (+ 2 descriptors and their ids of padding: the kernel reads the ids two sub-batches ahead)
+  FIA_HIP_TRY(X.gsdesc.reserve(sizeof(int2) * (size_t)(nd + 2), s));
+  FIA_HIP_TRY(X.gsids.reserve(sizeof(int32_t) * (size_t)((nd + 2) * kGsSub), s));
+  FIA_HIP_TRY(X.gswave.reserve(sizeof(int32_t) * wave.size(), s));
+  FIA_HIP_TRY(hipMemsetAsync(X.gsids.ptr, 0xff, sizeof(int32_t) * (size_t)((nd + 2) * kGsSub), s));
+  DevBuf dpos;
+  FIA_HIP_TRY(dpos.reserve(sizeof(int32_t) * (size_t)(nd + 1), s));
+  if (nd > 0) {
+    FIA_HIP_TRY(hipMemcpyAsync(X.gsdesc.ptr, desc.data(), sizeof(int2) * (size_t)nd, hipMemcpyHostToDevice, s));
+    FIA_HIP_TRY(hipMemcpyAsync(dpos.ptr, pos.data(), sizeof(int32_t) * (size_t)nd, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_gs_ids, dim3(grid_for(nd * kGsSub, 256)), dim3(256), 0, s, nd, X.gsdesc.as<int2>(),
+                       dpos.as<int32_t>(), X.side[0].other.as<int32_t>(), X.side[1].other.as<int32_t>(),
+                       X.gsids.as<int32_t>());
+    FIA_HIP_TRY(hipGetLastError());
+  }
+  FIA_HIP_TRY(hipMemsetAsync(X.gsdesc.as<int2>() + nd, 0, sizeof(int2) * 2, s));
+  FIA_HIP_TRY(hipMemcpyAsync(X.gswave.ptr, wave.data(), sizeof(int32_t) * wave.size(), hipMemcpyHostToDevice, s));
+  for (int sd = 0; sd < 2; ++sd) {
+    X.n_gscomb[sd] = (int64_t)comb[sd].size() / 4;
+    if (!comb[sd].empty()) {
+      FIA_HIP_TRY(X.gscomb[sd].reserve(sizeof(int32_t) * comb[sd].size(), s));
+      FIA_HIP_TRY(hipMemcpyAsync(X.gscomb[sd].ptr, comb[sd].data(), sizeof(int32_t) * comb[sd].size(),
+                                 hipMemcpyHostToDevice, s));
+    }
+  }
+  dpos.release(s);
+  FIA_HIP_TRY(hipStreamSynchronize(s));   // the host vectors go out of scope
+  X.gs_version = X.version;
+  return hipSuccess;
+}
+
 hipError_t build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* user, const int32_t* item,
                        const float* rating, hipStream_t s, std::string& why) {
   Index& X = c->idx;
