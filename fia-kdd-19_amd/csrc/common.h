@@ -36,7 +36,8 @@ constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
 constexpr int kGsSub = 16;              // ratings per Gram-stream sub-batch (4 f64 MFMA row-quads)
 constexpr int kGsSlice = 512;           // longest Gram-stream segment (longer lists: partial slices)
-constexpr int kGsTarget = 32;           // sub-batches per Gram-stream wave (at most 64: one per lane)
+constexpr int kGsTarget = 16;           // sub-batches per Gram-stream wave (a range closes at >= this)
+constexpr int kGsMaxSub = 60;           // most sub-batches of one wave's range (a multiple of 4; < 64 lanes)
 constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
 constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
@@ -321,6 +322,20 @@ struct PhaseSpan {
   hipEvent_t a = nullptr, b = nullptr;
 };
 struct QueryArgs;
+// MF k <= 16 Gram caches from the Gram stream (gram_mf.hip)
+struct GramStreamArgs {
+  const int2* desc;        // {meta, slot} per sub-batch (Index::gsdesc)
+  const int32_t* ids;      // other-side ids, kGsSub per sub-batch (quad-transposed), -1 past a list's end
+  const int32_t* wave;     // first descriptor of each wave's range [n_waves + 1]
+  int64_t n_waves;
+  const float* emb_other[2];
+  uint32_t bytes_other[2]; // their sizes (buffer ranges: a gather outside reads 0)
+  double* gram[2];
+  double* part[2];
+  const uint8_t* mark;     // fia_prepare_for: entities to build (users [0, U), items [U, U + I)), or null
+  int64_t moff[2];
+};
+hipError_t launch_gram_mf_stream(int k, const GramStreamArgs& G, hipStream_t s);
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t Q,
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,

@@ -1,0 +1,150 @@
+// MF k <= 16 entity Gram caches (the headline's prepare).  Reference: the restricted Hessian
+// of total_loss over the related batch (matrix_factorization.py:288-308, 324-351) restated per
+// entity, A_e = sum over e's list of g g^T with g = [other-side embedding ; 1].
+#include "kern.h"
+
+namespace fia {
+namespace {
+
+// raw buffer resource word 3 (gfx9 family)
+constexpr int kRsrcWord3 = 0x00020000;
+
+// ------------------------------------------------------------------------------------
+// The lists of both sides are cut into sub-batches of 16 ratings (build_gram_stream): a wave
+// walks the sub-batches of its range -- whole short lists one after another, or one
+// 512-rating slice of a long list -- with one v_mfma_f64_16x16x4_f64 per row-quad (4 per
+// sub-batch: a list costs ceil(len / 4) MFMAs, not a padded 64-row batch), and flushes an
+// entity's Gram when its last sub-batch is in.  The range's other-side ids go to LDS once
+// (stream order, quad-transposed: one 16-B LDS read gives a row group its 4 quad ids, and no
+// id load sits in front of a gather in the in-order vmcnt queue); the gathered rows run two
+// sub-batches ahead of the MFMAs in a 4-slot register ring.  A flush stages the packed
+// triangle (+ the bias row: column sums, the count) in LDS and writes it as 16-B stores.
+// fia_prepare_for marks: the sub-batches of unmarked entities are skipped (their gathers read
+// the zero row, no MFMA, no flush).
+// Lane map (f64 16x16x4): lane l supplies G[l >> 4][l & 15] of the row-quad as both A (= G^T)
+// and B; C register r = C[(l >> 4) + 4 r][l & 15].
+// ------------------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
+  static_assert(!M::ncf && M::K <= 16, "MF k <= 16");
+  constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  __shared__ __attribute__((aligned(16))) double stage[GSP];
+  __shared__ int4 sids[kGsMaxSub * 4];     // [sub-batch][row group] -> the group's 4 quad ids
+  const int64_t w = blockIdx.x;
+  if (w >= G.n_waves) return;
+  const int d0 = G.wave[w], nd = G.wave[w + 1] - d0;     // a multiple of 4, <= kGsMaxSub
+  const int lane = threadIdx.x;
+  const int col = lane & 15, grp = lane >> 4;
+  // the range's descriptors, one per lane; skipped: padding dummies and unmarked entities
+  const int2 dv = lane < nd ? G.desc[d0 + lane] : int2{1 << 7, -1};
+  bool sk = (dv.x >> 7) & 1;
+  if (G.mark) sk = sk || !G.mark[G.moff[(dv.x >> 6) & 1] + (dv.x >> 8)];
+  const uint64_t skipm = __ballot(sk);
+  {
+    const int4* __restrict__ src = reinterpret_cast<const int4*>(G.ids) + (int64_t)d0 * 4;
+    int4 tmp[kGsMaxSub * 4 / 64];
+#pragma unroll
+    for (int r = 0; r < kGsMaxSub * 4 / 64; ++r) {
+      const int i = r * 64 + lane;
+      tmp[r] = src[i < nd * 4 ? i : 0];
+    }
+#pragma unroll
+    for (int r = 0; r < kGsMaxSub * 4 / 64; ++r) sids[r * 64 + lane] = tmp[r];
+    wave_lds_sync();
+  }
+  // rows of sub-batch t: quad q, row group grp -> rating 4 q + grp of the sub-batch
+  // Masked lanes (past a list's end, skipped sub-batches, columns >= k) gather at an offset
+  // outside the table's buffer range, which the hardware answers with 0 -- no select on the
+  // loaded value (a use that would make the compiler wait for the load where it sits)
+  const __amdgpu_buffer_rsrc_t rs0 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.emb_other[0]), 0, G.bytes_other[0], kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t rs1 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.emb_other[1]), 0, G.bytes_other[1], kRsrcWord3);
+  auto rows = [&](int t, float (&v)[4]) {
+    const int meta = __builtin_amdgcn_readlane(dv.x, t);
+    const bool skt = (skipm >> t) & 1;
+    const __amdgpu_buffer_rsrc_t rs = (meta >> 6) & 1 ? rs1 : rs0;
+    const int4 o4 = sids[(t < nd ? t : 0) * 4 + grp];
+    const int32_t oq[4] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool ok = oq[q] >= 0 && !skt && col < K;
+      const unsigned off = ok ? (unsigned)(oq[q] * K + col) * 4u : 0xfffffff0u;
+      v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0));
+    }
+  };
+  d4_t acc = {0.0, 0.0, 0.0, 0.0};
+  double sum = 0.0;
+  int cnt = 0;
+  auto step = [&](int t, const float (&vin)[4]) {
+    const int meta = __builtin_amdgcn_readlane(dv.x, t);
+    // the slot's values pass an empty asm here: the converts (and the wait for the gathers)
+    // stay at this sub-batch instead of being hoisted to the loop head with the others
+    float v[4] = {vin[0], vin[1], vin[2], vin[3]};
+    asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+    double g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = (double)v[q];
+    // (a skipped sub-batch gathered zeros: its MFMAs add nothing, no branch around them)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(g[q], g[q], acc, 0, 0, 0);
+    sum += (g[0] + g[1]) + (g[2] + g[3]);
+    const bool skt = (skipm >> t) & 1;
+    cnt += skt ? 0 : meta & 31;
+    if (skt || !((meta >> 5) & 1)) return;
+    // the entity's (or the slice's) Gram: packed lower triangle, bias row, count
+    const int slot = __builtin_amdgcn_readlane(dv.y, t);
+    const int sd = (meta >> 6) & 1, e = meta >> 8;
+    double cs = sum;
+    cs += __shfl_xor(cs, 16);
+    cs += __shfl_xor(cs, 32);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = grp + 4 * rr;
+      if (row < K && col <= row) stage[tri(row, col)] = acc[rr];
+    }
+    if (grp == 0 && col < K) stage[tri(K, col)] = cs;
+    if (lane == 0) stage[tri(K, K)] = (double)cnt;
+    if (GSP > GS && lane == 1) stage[GSP - 1] = 0.0;
+    wave_lds_sync();
+    double* __restrict__ out = slot < 0 ? G.gram[sd] + (int64_t)e * GSP : G.part[sd] + (int64_t)slot * GSP;
+#pragma unroll
+    for (int b = 0; b < GSP; b += 128)
+      if (b + 2 * lane < GSP)
+        *reinterpret_cast<double2*>(out + b + 2 * lane) = *reinterpret_cast<const double2*>(&stage[b + 2 * lane]);
+    wave_lds_sync();
+    acc = d4_t{0.0, 0.0, 0.0, 0.0};
+    sum = 0.0;
+    cnt = 0;
+  };
+  // four-slot ring, gathers two sub-batches ahead of the MFMAs (slots named statically: the
+  // loop runs four sub-batches per trip; past the range's end the gathers are skipped ones)
+  float r0[4], r1[4], r2[4], r3[4];
+  rows(0, r0);
+  rows(1, r1);
+  for (int t = 0; t < nd; t += 4) {
+    rows(t + 2, r2);
+    step(t, r0);
+    rows(t + 3, r3);
+    step(t + 1, r1);
+    rows(t + 4, r0);
+    step(t + 2, r2);
+    rows(t + 5, r1);
+    step(t + 3, r3);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_gram_mf_stream(int k, const GramStreamArgs& G, hipStream_t s) {
+  if (G.n_waves <= 0) return hipSuccess;
+  if (k == 16)
+    hipLaunchKernelGGL(k_gram_mf_stream<MFm<16>>, dim3((unsigned)G.n_waves), dim3(64), 0, s, G);
+  else if (k == 8)
+    hipLaunchKernelGGL(k_gram_mf_stream<MFm<8>>, dim3((unsigned)G.n_waves), dim3(64), 0, s, G);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace fia

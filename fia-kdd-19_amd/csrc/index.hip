@@ -580,15 +580,16 @@ hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s) {
   return hipSuccess;
 }
 
-// the other-side ids of the Gram stream, in stream order: ids[kGsSub d + r] = other[side][pos_d + r]
-// for r < valid_d, else -1
+// the other-side ids of the Gram stream, in stream order and quad-transposed: rating 4 q + g of
+// sub-batch d at ids[kGsSub d + 4 g + q] (the 16 lanes of MFMA row group g read their four quads'
+// ids as one 16-B word), other[side][pos_d + 4 q + g], -1 past the list's end
 __global__ void k_gs_ids(int64_t nd, const int2* __restrict__ desc, const int32_t* __restrict__ pos,
                          const int32_t* __restrict__ other0, const int32_t* __restrict__ other1,
                          int32_t* __restrict__ ids) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nd * kGsSub;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t d = t / kGsSub;
-    const int r = (int)(t % kGsSub);
+    const int r = 4 * (int)(t & 3) + (int)((t >> 2) & 3);   // t % 16 = 4 g + q  ->  rating 4 q + g
     const int meta = desc[d].x;
     const int valid = meta & 31, side = (meta >> 6) & 1;
     ids[t] = r < valid ? (side ? other1 : other0)[pos[d] + r] : -1;
@@ -627,7 +628,7 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   std::vector<int32_t> pos, wave{0};
   int cur = 0;
   auto close_wave = [&]() {
-    if (cur & 1) {   // an even count per wave (the kernel runs two sub-batches per loop trip)
+    while (cur & 3) {   // a multiple of 4 per wave (the kernel runs four sub-batches per loop trip)
       desc.push_back(int2{1 << 7, -1});
       pos.push_back(0);
       ++cur;
@@ -637,7 +638,7 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   };
   for (const Seg& g : segs) {
     const int nsb = g.len == 0 ? 1 : (int)((g.len + kGsSub - 1) / kGsSub);
-    if (cur > 0 && cur + nsb > 62) close_wave();
+    if (cur > 0 && cur + nsb > kGsMaxSub - 4) close_wave();
     for (int t = 0; t < nsb; ++t) {
       const int valid = (int)std::min<int64_t>(kGsSub, g.len - (int64_t)t * kGsSub);
       const int meta = (valid < 0 ? 0 : valid) | (t == nsb - 1 ? 1 << 5 : 0) | (g.side << 6) | (g.e << 8);
@@ -651,7 +652,6 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   const int64_t nd = (int64_t)desc.size();
   X.n_gsdesc = nd;
   X.n_gsw = (int64_t)wave.size() - 1;
-  // (+ 2 descriptors and their ids of padding: the kernel reads the ids two sub-batches ahead)
   FIA_HIP_TRY(X.gsdesc.reserve(sizeof(int2) * (size_t)(nd + 2), s));
   FIA_HIP_TRY(X.gsids.reserve(sizeof(int32_t) * (size_t)((nd + 2) * kGsSub), s));
   FIA_HIP_TRY(X.gswave.reserve(sizeof(int32_t) * wave.size(), s));

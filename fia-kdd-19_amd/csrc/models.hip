@@ -1557,114 +1557,6 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
 }
 
 // ------------------------------------------------------------------------------------
-// MF k <= 16 Gram caches as one stream (the headline's prepare; mf:288-308 / 324-351 restated
-// per entity: A_e = sum over e's list of g g^T, g = [other embedding ; 1]).  The lists of both
-// sides are cut into sub-batches of 16 ratings (build_gram_stream): a wave walks the
-// sub-batches of its range -- whole short lists one after another, or one 512-rating slice of a
-// long list -- with one v_mfma_f64_16x16x4_f64 per row-quad (4 per sub-batch: a list costs
-// ceil(len / 4) MFMAs, not a padded 64-row batch), and flushes an entity's Gram when its last
-// sub-batch is in.  Software pipeline, two sub-batches per loop trip: the other-side ids of
-// sub-batch t + 2 (stream order, one coalesced 64-B load) and the gathered rows of t + 1 are in
-// flight while the MFMAs of t run.  A flush stages the packed triangle (+ the bias row: column
-// sums, the count) in LDS and writes it as 16-B stores.  fia_prepare_for marks: the sub-batches
-// of unmarked entities are skipped (their gathers read row 0, no MFMA, no flush).
-// Lane map (f64 16x16x4): lane l supplies G[l >> 4][l & 15] of the row-quad as both A (= G^T)
-// and B; C register r = C[(l >> 4) + 4 r][l & 15].
-// ------------------------------------------------------------------------------------
-struct GramStream {
-  const int2* desc;        // {meta, slot} per sub-batch (Index::gsdesc)
-  const int32_t* ids;      // other-side ids, kGsSub per sub-batch, -1 past a list's end
-  const int32_t* wave;     // first descriptor of each wave's range [n_waves + 1]
-  int64_t n_waves;
-  const float* emb_other[2];
-  double* gram[2];
-  double* part[2];
-  const uint8_t* mark;
-  int64_t moff[2];
-};
-
-template <class M>
-__global__ __launch_bounds__(64) void k_gram_mf_stream(GramStream G) {
-  static_assert(!M::ncf && M::K <= 16, "MF k <= 16");
-  constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
-  __shared__ __attribute__((aligned(16))) double stage[GSP];
-  const int64_t w = blockIdx.x;
-  if (w >= G.n_waves) return;
-  const int d0 = G.wave[w], nd = G.wave[w + 1] - d0;     // even, <= 62
-  const int lane = threadIdx.x;
-  const int col = lane & 15, grp = lane >> 4;
-  // the range's descriptors, one per lane; skipped: padding dummies and unmarked entities
-  const int2 dv = lane < nd ? G.desc[d0 + lane] : int2{1 << 7, -1};
-  bool sk = (dv.x >> 7) & 1;
-  if (G.mark) sk = sk || !G.mark[G.moff[(dv.x >> 6) & 1] + (dv.x >> 8)];
-  const uint64_t skipm = __ballot(sk);
-  const int32_t* __restrict__ idsw = G.ids + (int64_t)d0 * kGsSub + (lane & 15);
-  // rows of sub-batch t: quad q, row group grp -> rating 4 q + grp of the sub-batch
-  auto rows = [&](int32_t idv, int t, float (&v)[4]) {
-    const int meta = __builtin_amdgcn_readlane(dv.x, t);
-    const bool skt = (skipm >> t) & 1;
-    const float* __restrict__ T = G.emb_other[(meta >> 6) & 1];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int32_t o = __shfl(idv, 4 * q + grp);
-      const bool ok = o >= 0 && !skt && col < K;
-      const float x = T[(int64_t)(ok ? o : 0) * K + (col < K ? col : 0)];
-      v[q] = ok ? x : 0.f;
-    }
-  };
-  d4_t acc = {0.0, 0.0, 0.0, 0.0};
-  double sum = 0.0;
-  int cnt = 0;
-  auto step = [&](int t, const float (&v)[4]) {
-    if ((skipm >> t) & 1) return;
-    const int meta = __builtin_amdgcn_readlane(dv.x, t);
-    double g[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) g[q] = (double)v[q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(g[q], g[q], acc, 0, 0, 0);
-    sum += (g[0] + g[1]) + (g[2] + g[3]);
-    cnt += meta & 31;
-    if (!((meta >> 5) & 1)) return;
-    // the entity's (or the slice's) Gram: packed lower triangle, bias row, count
-    const int slot = __builtin_amdgcn_readlane(dv.y, t);
-    const int sd = (meta >> 6) & 1, e = meta >> 8;
-    double cs = sum;
-    cs += __shfl_xor(cs, 16);
-    cs += __shfl_xor(cs, 32);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = grp + 4 * rr;
-      if (row < K && col <= row) stage[tri(row, col)] = acc[rr];
-    }
-    if (grp == 0 && col < K) stage[tri(K, col)] = cs;
-    if (lane == 0) stage[tri(K, K)] = (double)cnt;
-    if (GSP > GS && lane == 1) stage[GSP - 1] = 0.0;
-    wave_lds_sync();
-    double* __restrict__ out = slot < 0 ? G.gram[sd] + (int64_t)e * GSP : G.part[sd] + (int64_t)slot * GSP;
-#pragma unroll
-    for (int b = 0; b < GSP; b += 128)
-      if (b + 2 * lane < GSP)
-        *reinterpret_cast<double2*>(out + b + 2 * lane) = *reinterpret_cast<const double2*>(&stage[b + 2 * lane]);
-    wave_lds_sync();
-    acc = d4_t{0.0, 0.0, 0.0, 0.0};
-    sum = 0.0;
-    cnt = 0;
-  };
-  int32_t idA = idsw[0], idB = idsw[kGsSub];
-  float rA[4], rB[4];
-  rows(idA, 0, rA);
-  for (int t = 0; t < nd; t += 2) {
-    rows(idB, t + 1, rB);
-    idA = idsw[(t + 2) * kGsSub];
-    step(t, rA);
-    rows(idA, t + 2 < nd ? t + 2 : t, rA);
-    idB = idsw[(t + 3) * kGsSub];
-    step(t + 1, rB);
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // NCF per list position + entity Gram, one pass (ncf:102-145, TF ReluGrad masks).  A wave
 // takes one work item (<= gchunk positions of one entity's list, both sides in one
 // launch) in slabs of 16 positions p, e = the entity, o = other(p):
@@ -2850,6 +2742,7 @@ constexpr int kRunLambda = 16;
 // MF k <= 16: the Gram stream (its descriptors carry the entity in 24 bits)
 template <class M>
 bool use_gram_stream(const int64_t (&n_ent)[2]) {
+  // (and a table's bytes in a 32-bit buffer range)
   return !M::ncf && M::K <= 16 && n_ent[0] < (1 << 23) && n_ent[1] < (1 << 23);
 }
 
@@ -2924,25 +2817,21 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
     FIA_HIP_TRY(build_gram_stream(c, s));
     for (int sd = 0; sd < 2; ++sd)
       if (X.n_gsslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gsslots[sd] * GSP), s));
-    GramStream GT{};
+    GramStreamArgs GT{};
     GT.desc = X.gsdesc.as<int2>();
     GT.ids = X.gsids.as<int32_t>();
     GT.wave = X.gswave.as<int32_t>();
     GT.n_waves = X.n_gsw;
     for (int sd = 0; sd < 2; ++sd) {
       GT.emb_other[sd] = c->p.t[sd == 0 ? 1 : 0];
+      GT.bytes_other[sd] = (uint32_t)(n_ent[1 - sd] * K * (int64_t)sizeof(float));
       GT.gram[sd] = c->gram[sd].as<double>();
       GT.part[sd] = c->gpart[sd].as<double>();
     }
     GT.mark = mark;
     GT.moff[0] = 0;
     GT.moff[1] = n_ent[0];
-    if constexpr (!M::ncf && M::K <= 16) {
-      if (X.n_gsw > 0) {
-        hipLaunchKernelGGL(k_gram_mf_stream<M>, dim3((unsigned)X.n_gsw), dim3(64), 0, s, GT);
-        FIA_HIP_TRY(hipGetLastError());
-      }
-    }
+    if (X.n_gsw > 0) FIA_HIP_TRY(launch_gram_mf_stream(M::K, GT, s));
     const int64_t nc0 = X.n_gscomb[0], nc1 = X.n_gscomb[1];
     if (nc0 + nc1 > 0) {
       hipLaunchKernelGGL(k_gram_combine, dim3((unsigned)(nc0 + nc1)), dim3(256), 0, s, nc0, X.gscomb[0].as<int32_t>(),
