@@ -35,9 +35,10 @@ constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
 constexpr int kGsSub = 16;              // ratings per Gram-stream sub-batch (4 f64 MFMA row-quads)
-constexpr int kGsSlice = 512;           // longest Gram-stream segment (longer lists: partial slices)
-constexpr int kGsTarget = 16;           // sub-batches per Gram-stream wave (a range closes at >= this)
-constexpr int kGsMaxSub = 60;           // most sub-batches of one wave's range (a multiple of 4; < 64 lanes)
+constexpr int kGsSlice = 256;           // longest Gram-stream segment (longer lists: partial slices)
+constexpr int kGsTarget = 8;            // sub-batches per Gram-stream wave (a range closes at >= this)
+constexpr int kGsRing = 8;              // gathered sub-batches in the kernel's register ring
+constexpr int kGsMaxSub = 48;           // most sub-batches of one wave's range (a multiple of kGsRing)
 constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
 constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)

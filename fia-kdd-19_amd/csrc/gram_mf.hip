@@ -73,10 +73,13 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
       v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0));
     }
   };
-  d4_t acc = {0.0, 0.0, 0.0, 0.0};
+  // two accumulators (even / odd row-quads): consecutive MFMAs are independent
+  d4_t acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
   double sum = 0.0;
   int cnt = 0;
   auto step = [&](int t, const float (&vin)[4]) {
+    // skipped sub-batches (padding, unmarked entities) gathered zeros and end no segment
+    if ((skipm >> t) & 1) return;
     const int meta = __builtin_amdgcn_readlane(dv.x, t);
     // the slot's values pass an empty asm here: the converts (and the wait for the gathers)
     // stay at this sub-batch instead of being hoisted to the loop head with the others
@@ -85,13 +88,13 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
     double g[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) g[q] = (double)v[q];
-    // (a skipped sub-batch gathered zeros: its MFMAs add nothing, no branch around them)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(g[q], g[q], acc, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(g[0], g[0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(g[1], g[1], acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(g[2], g[2], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(g[3], g[3], acc1, 0, 0, 0);
     sum += (g[0] + g[1]) + (g[2] + g[3]);
-    const bool skt = (skipm >> t) & 1;
-    cnt += skt ? 0 : meta & 31;
-    if (skt || !((meta >> 5) & 1)) return;
+    cnt += meta & 31;
+    if (!((meta >> 5) & 1)) return;
     // the entity's (or the slice's) Gram: packed lower triangle, bias row, count
     const int slot = __builtin_amdgcn_readlane(dv.y, t);
     const int sd = (meta >> 6) & 1, e = meta >> 8;
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = grp + 4 * rr;
-      if (row < K && col <= row) stage[tri(row, col)] = acc[rr];
+      if (row < K && col <= row) stage[tri(row, col)] = acc0[rr] + acc1[rr];
     }
     if (grp == 0 && col < K) stage[tri(K, col)] = cs;
     if (lane == 0) stage[tri(K, K)] = (double)cnt;
@@ -113,24 +116,24 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
       if (b + 2 * lane < GSP)
         *reinterpret_cast<double2*>(out + b + 2 * lane) = *reinterpret_cast<const double2*>(&stage[b + 2 * lane]);
     wave_lds_sync();
-    acc = d4_t{0.0, 0.0, 0.0, 0.0};
+    acc0 = acc1 = d4_t{0.0, 0.0, 0.0, 0.0};
     sum = 0.0;
     cnt = 0;
   };
-  // four-slot ring, gathers two sub-batches ahead of the MFMAs (slots named statically: the
-  // loop runs four sub-batches per trip; past the range's end the gathers are skipped ones)
-  float r0[4], r1[4], r2[4], r3[4];
-  rows(0, r0);
-  rows(1, r1);
-  for (int t = 0; t < nd; t += 4) {
-    rows(t + 2, r2);
-    step(t, r0);
-    rows(t + 3, r3);
-    step(t + 1, r1);
-    rows(t + 4, r0);
-    step(t + 2, r2);
-    rows(t + 5, r1);
-    step(t + 3, r3);
+  // kGsRing-slot register ring, gathers kGsRing - 2 sub-batches ahead of the MFMAs (slots
+  // named statically: one ring turn per loop trip; past the range's end the gathers are
+  // skipped ones)
+  static_assert(kGsRing == 8 && kGsMaxSub % kGsRing == 0, "ring of 8");
+  constexpr int AH = kGsRing - 2;
+  float r[kGsRing][4];
+#pragma unroll
+  for (int j = 0; j < AH; ++j) rows(j, r[j]);
+  for (int t = 0; t < nd; t += kGsRing) {
+#pragma unroll
+    for (int j = 0; j < kGsRing; ++j) {
+      rows(t + j + AH, r[(j + AH) % kGsRing]);
+      step(t + j, r[j]);
+    }
   }
 }
 

@@ -628,7 +628,7 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   std::vector<int32_t> pos, wave{0};
   int cur = 0;
   auto close_wave = [&]() {
-    while (cur & 3) {   // a multiple of 4 per wave (the kernel runs four sub-batches per loop trip)
+    while (cur % kGsRing) {   // a multiple of the ring per wave (one ring turn per loop trip)
       desc.push_back(int2{1 << 7, -1});
       pos.push_back(0);
       ++cur;
@@ -638,7 +638,7 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   };
   for (const Seg& g : segs) {
     const int nsb = g.len == 0 ? 1 : (int)((g.len + kGsSub - 1) / kGsSub);
-    if (cur > 0 && cur + nsb > kGsMaxSub - 4) close_wave();
+    if (cur > 0 && cur + nsb > kGsMaxSub - kGsRing) close_wave();
     for (int t = 0; t < nsb; ++t) {
       const int valid = (int)std::min<int64_t>(kGsSub, g.len - (int64_t)t * kGsSub);
       const int meta = (valid < 0 ? 0 : valid) | (t == nsb - 1 ? 1 << 5 : 0) | (g.side << 6) | (g.e << 8);
