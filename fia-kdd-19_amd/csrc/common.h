@@ -36,7 +36,9 @@ constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
 constexpr int kGsSub = 16;              // ratings per Gram-stream sub-batch (4 f64 MFMA row-quads)
 constexpr int kGsSlice = 256;           // longest Gram-stream segment (longer lists: partial slices)
-constexpr int kGsTarget = 8;            // sub-batches per Gram-stream wave (a range closes at >= this)
+constexpr int kGsTarget = 16;           // sub-batches per Gram-stream wave (a range closes at >= this)
+constexpr uint32_t kGsNoRow = 0x7fffff00u;   // Gram-stream row offset of no rating: outside any
+                                             // table's buffer range, even + a lane's column bytes
 constexpr int kGsRing = 8;              // gathered sub-batches in the kernel's register ring
 constexpr int kGsMaxSub = 48;           // most sub-batches of one wave's range (a multiple of kGsRing)
 constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
@@ -112,14 +114,16 @@ struct Index {
   std::vector<int32_t> hord[2];   // entities by list length, longest first (host)
   int64_t gchunk = 0;             // list rows per small-k Gram work item of gitems
   // MF k <= 16 Gram stream (build_gram_stream, k_gram_mf_stream): the lists of both sides cut
-  // into sub-batches of kGsSub ratings, one descriptor each {meta, slot} (meta = valid ratings
-  // | last of its segment << 5 | side << 6 | dummy << 7 | entity << 8), their other-side ids
-  // in stream order (kGsSub per sub-batch, -1 past a list's end), and the first descriptor of
-  // every wave's range (whole lists up to kGsSlice ratings, longer lists in kGsSlice slices
-  // whose partial Grams gscomb sums in slot order)
+  // into sub-batches of kGsSub ratings, one descriptor each {meta, out} (meta = valid ratings
+  // | last of its segment << 5 | side << 6 | dummy << 7 | entity << 8; out, on a segment's last
+  // sub-batch: its rating count << 23 | partial slot + 1, 0 = the entity's own Gram), the byte
+  // offsets of their other-side rows in stream order (kGsSub per sub-batch, kGsNoRow past a
+  // list's end), and the first descriptor of every wave's range (whole lists up to kGsSlice
+  // ratings, longer lists in kGsSlice slices whose partial Grams gscomb sums in slot order)
   DevBuf gsdesc, gsids, gswave, gscomb[2];
   int64_t n_gsw = 0, n_gsdesc = 0, n_gscomb[2] = {0, 0}, n_gsslots[2] = {0, 0};
   uint64_t gs_version = ~0ull;
+  int gs_k = 0;
   uint64_t version = 0;           // bumped by every build_index
   bool valid = false;
 };
@@ -278,7 +282,7 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
                         bool runs = false, int slice_cost = 0);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
 // the MF k <= 16 Gram stream of the current index (Index::gs*), rebuilt after build_index
-hipError_t build_gram_stream(fia_ctx* c, hipStream_t s);
+hipError_t build_gram_stream(fia_ctx* c, int k, hipStream_t s);
 // per-batch query groups + entity-chunk work items (needs build_chunks' coff first)
 hipError_t build_groups(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_items, int qb, hipStream_t s, int cpi = 1);
@@ -326,7 +330,7 @@ struct QueryArgs;
 // MF k <= 16 Gram caches from the Gram stream (gram_mf.hip)
 struct GramStreamArgs {
   const int2* desc;        // {meta, slot} per sub-batch (Index::gsdesc)
-  const int32_t* ids;      // other-side ids, kGsSub per sub-batch (quad-transposed), -1 past a list's end
+  const uint32_t* ids;     // other-side row byte offsets, kGsSub per sub-batch (quad-transposed)
   const int32_t* wave;     // first descriptor of each wave's range [n_waves + 1]
   int64_t n_waves;
   const float* emb_other[2];

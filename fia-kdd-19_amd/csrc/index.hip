@@ -580,25 +580,26 @@ hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s) {
   return hipSuccess;
 }
 
-// the other-side ids of the Gram stream, in stream order and quad-transposed: rating 4 q + g of
-// sub-batch d at ids[kGsSub d + 4 g + q] (the 16 lanes of MFMA row group g read their four quads'
-// ids as one 16-B word), other[side][pos_d + 4 q + g], -1 past the list's end
+// the other-side rows of the Gram stream as byte offsets into their table (id * k * 4), in
+// stream order and quad-transposed: rating 4 q + g of sub-batch d at ids[kGsSub d + 4 g + q]
+// (the 16 lanes of MFMA row group g read their four quads' offsets as one 16-B word),
+// kGsNoRow past the list's end
 __global__ void k_gs_ids(int64_t nd, const int2* __restrict__ desc, const int32_t* __restrict__ pos,
-                         const int32_t* __restrict__ other0, const int32_t* __restrict__ other1,
-                         int32_t* __restrict__ ids) {
+                         const int32_t* __restrict__ other0, const int32_t* __restrict__ other1, int k,
+                         uint32_t* __restrict__ ids) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nd * kGsSub;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t d = t / kGsSub;
     const int r = 4 * (int)(t & 3) + (int)((t >> 2) & 3);   // t % 16 = 4 g + q  ->  rating 4 q + g
     const int meta = desc[d].x;
     const int valid = meta & 31, side = (meta >> 6) & 1;
-    ids[t] = r < valid ? (side ? other1 : other0)[pos[d] + r] : -1;
+    ids[t] = r < valid ? (uint32_t)(side ? other1 : other0)[pos[d] + r] * (uint32_t)(k * 4) : kGsNoRow;
   }
 }
 
-hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
+hipError_t build_gram_stream(fia_ctx* c, int k, hipStream_t s) {
   Index& X = c->idx;
-  if (X.gs_version == X.version && X.gswave.ptr) return hipSuccess;
+  if (X.gs_version == X.version && X.gs_k == k && X.gswave.ptr) return hipSuccess;
   struct Seg {
     int64_t len;
     int side;
@@ -641,8 +642,10 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
     if (cur > 0 && cur + nsb > kGsMaxSub - kGsRing) close_wave();
     for (int t = 0; t < nsb; ++t) {
       const int valid = (int)std::min<int64_t>(kGsSub, g.len - (int64_t)t * kGsSub);
-      const int meta = (valid < 0 ? 0 : valid) | (t == nsb - 1 ? 1 << 5 : 0) | (g.side << 6) | (g.e << 8);
-      desc.push_back(int2{meta, g.slot});
+      const bool last = t == nsb - 1;
+      const int meta = (valid < 0 ? 0 : valid) | (last ? 1 << 5 : 0) | (g.side << 6) | (g.e << 8);
+      const uint32_t out = last ? ((uint32_t)g.len << 23) | (uint32_t)(g.slot + 1) : 0u;
+      desc.push_back(int2{meta, (int)out});
       pos.push_back((int32_t)(X.hptr[g.side][(size_t)g.e] + g.start + (int64_t)t * kGsSub));
     }
     cur += nsb;
@@ -655,15 +658,14 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   FIA_HIP_TRY(X.gsdesc.reserve(sizeof(int2) * (size_t)(nd + 2), s));
   FIA_HIP_TRY(X.gsids.reserve(sizeof(int32_t) * (size_t)((nd + 2) * kGsSub), s));
   FIA_HIP_TRY(X.gswave.reserve(sizeof(int32_t) * wave.size(), s));
-  FIA_HIP_TRY(hipMemsetAsync(X.gsids.ptr, 0xff, sizeof(int32_t) * (size_t)((nd + 2) * kGsSub), s));
   DevBuf dpos;
   FIA_HIP_TRY(dpos.reserve(sizeof(int32_t) * (size_t)(nd + 1), s));
   if (nd > 0) {
     FIA_HIP_TRY(hipMemcpyAsync(X.gsdesc.ptr, desc.data(), sizeof(int2) * (size_t)nd, hipMemcpyHostToDevice, s));
     FIA_HIP_TRY(hipMemcpyAsync(dpos.ptr, pos.data(), sizeof(int32_t) * (size_t)nd, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_gs_ids, dim3(grid_for(nd * kGsSub, 256)), dim3(256), 0, s, nd, X.gsdesc.as<int2>(),
-                       dpos.as<int32_t>(), X.side[0].other.as<int32_t>(), X.side[1].other.as<int32_t>(),
-                       X.gsids.as<int32_t>());
+                       dpos.as<int32_t>(), X.side[0].other.as<int32_t>(), X.side[1].other.as<int32_t>(), k,
+                       X.gsids.as<uint32_t>());
     FIA_HIP_TRY(hipGetLastError());
   }
   FIA_HIP_TRY(hipMemsetAsync(X.gsdesc.as<int2>() + nd, 0, sizeof(int2) * 2, s));
@@ -679,6 +681,7 @@ hipError_t build_gram_stream(fia_ctx* c, hipStream_t s) {
   dpos.release(s);
   FIA_HIP_TRY(hipStreamSynchronize(s));   // the host vectors go out of scope
   X.gs_version = X.version;
+  X.gs_k = k;
   return hipSuccess;
 }
 

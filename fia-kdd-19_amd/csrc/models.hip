@@ -2814,12 +2814,12 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
     }
   } else if (use_gram_stream<M>(n_ent)) {
     // MF k <= 16: the Gram stream (both sides, one launch), then the partial slices combined
-    FIA_HIP_TRY(build_gram_stream(c, s));
+    FIA_HIP_TRY(build_gram_stream(c, K, s));
     for (int sd = 0; sd < 2; ++sd)
       if (X.n_gsslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gsslots[sd] * GSP), s));
     GramStreamArgs GT{};
     GT.desc = X.gsdesc.as<int2>();
-    GT.ids = X.gsids.as<int32_t>();
+    GT.ids = X.gsids.as<uint32_t>();
     GT.wave = X.gswave.as<int32_t>();
     GT.n_waves = X.n_gsw;
     for (int sd = 0; sd < 2; ++sd) {
