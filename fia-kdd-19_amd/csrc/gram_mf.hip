@@ -33,7 +33,7 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
   static_assert(!M::ncf && M::K <= 16, "MF k <= 16");
   constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   static_assert(kGsRing == 8 && kGsMaxSub % kGsRing == 0 && kGsMaxSub + kGsRing <= 64, "ring of 8");
-  __shared__ __attribute__((aligned(16))) double stage[GSP];
+  __shared__ __attribute__((aligned(16))) double stage[kGsMaxSeg][GSP];
   __shared__ uint4 sids[kGsMaxSub * 4];     // [sub-batch][row group] -> the group's 4 row offsets
   const int64_t w = blockIdx.x;
   if (w >= G.n_waves) return;
@@ -78,6 +78,7 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
   // two accumulators (even / odd row-quads): consecutive MFMAs are independent
   d4_t acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
   double sum = 0.0;
+  int nseg = 0;                            // segments flushed so far (their Grams in stage[])
   auto step = [&](int t, const float (&vin)[4]) {
     if ((skipm >> t) & 1) return;
     // the slot's values pass an empty asm here: the converts (and the wait for the gathers)
@@ -93,28 +94,23 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
     acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(g[3], g[3], acc1, 0, 0, 0);
     sum += (g[0] + g[1]) + (g[2] + g[3]);
     if (!((lastm >> t) & 1)) return;
-    // the entity's (or the slice's) Gram: packed lower triangle, bias row, count
-    const int meta = __builtin_amdgcn_readlane(dv.x, t);
+    // the entity's (or the slice's) Gram -- packed lower triangle, bias row, count -- staged in
+    // LDS; the global stores wait for the end of the range (a store in the middle of the ring
+    // stalled the wave behind the gathers in flight: ~60 % of this kernel's time)
     const uint32_t out = (uint32_t)__builtin_amdgcn_readlane(dv.y, t);
-    const int sd = (meta >> 6) & 1, e = meta >> 8, slot = (int)(out & 0x7fffffu) - 1;
+    double* __restrict__ st = stage[nseg];
     double cs = sum;
     cs += __shfl_xor(cs, 16);
     cs += __shfl_xor(cs, 32);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = grp + 4 * rr;
-      if (row < K && col <= row) stage[tri(row, col)] = acc0[rr] + acc1[rr];
+      if (row < K && col <= row) st[tri(row, col)] = acc0[rr] + acc1[rr];
     }
-    if (grp == 0 && col < K) stage[tri(K, col)] = cs;
-    if (lane == 0) stage[tri(K, K)] = (double)(out >> 23);
-    if (GSP > GS && lane == 1) stage[GSP - 1] = 0.0;
-    wave_lds_sync();
-    double* __restrict__ o = slot < 0 ? G.gram[sd] + (int64_t)e * GSP : G.part[sd] + (int64_t)slot * GSP;
-#pragma unroll
-    for (int b = 0; b < GSP; b += 128)
-      if (b + 2 * lane < GSP)
-        *reinterpret_cast<double2*>(o + b + 2 * lane) = *reinterpret_cast<const double2*>(&stage[b + 2 * lane]);
-    wave_lds_sync();
+    if (grp == 0 && col < K) st[tri(K, col)] = cs;
+    if (lane == 0) st[tri(K, K)] = (double)(out >> 23);
+    if (GSP > GS && lane == 1) st[GSP - 1] = 0.0;
+    ++nseg;
     acc0 = acc1 = d4_t{0.0, 0.0, 0.0, 0.0};
     sum = 0.0;
   };
@@ -131,6 +127,22 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
       rows(t + j + AH, r[(j + AH) % kGsRing]);
       step(t + j, r[j]);
     }
+  }
+  // the range's Grams, in segment order: segment k ends at the k-th descriptor that is the last
+  // of a segment and not skipped
+  wave_lds_sync();
+  uint64_t ends = lastm & ~skipm;
+  for (int k = 0; k < nseg; ++k) {
+    const int t = (int)__builtin_ctzll(ends);
+    ends &= ends - 1;
+    const int meta = __builtin_amdgcn_readlane(dv.x, t);
+    const uint32_t out = (uint32_t)__builtin_amdgcn_readlane(dv.y, t);
+    const int sd = (meta >> 6) & 1, e = meta >> 8, slot = (int)(out & 0x7fffffu) - 1;
+    double* __restrict__ o = slot < 0 ? G.gram[sd] + (int64_t)e * GSP : G.part[sd] + (int64_t)slot * GSP;
+#pragma unroll
+    for (int b = 0; b < GSP; b += 128)
+      if (b + 2 * lane < GSP)
+        *reinterpret_cast<double2*>(o + b + 2 * lane) = *reinterpret_cast<const double2*>(&stage[k][b + 2 * lane]);
   }
 }
 

@@ -627,7 +627,7 @@ hipError_t build_gram_stream(fia_ctx* c, int k, hipStream_t s) {
   std::stable_sort(segs.begin(), segs.end(), [](const Seg& a, const Seg& b) { return a.len > b.len; });
   std::vector<int2> desc;
   std::vector<int32_t> pos, wave{0};
-  int cur = 0;
+  int cur = 0, nseg = 0;
   auto close_wave = [&]() {
     while (cur % kGsRing) {   // a multiple of the ring per wave (one ring turn per loop trip)
       desc.push_back(int2{1 << 7, -1});
@@ -636,6 +636,7 @@ hipError_t build_gram_stream(fia_ctx* c, int k, hipStream_t s) {
     }
     wave.push_back((int32_t)desc.size());
     cur = 0;
+    nseg = 0;
   };
   for (const Seg& g : segs) {
     const int nsb = g.len == 0 ? 1 : (int)((g.len + kGsSub - 1) / kGsSub);
@@ -649,7 +650,7 @@ hipError_t build_gram_stream(fia_ctx* c, int k, hipStream_t s) {
       pos.push_back((int32_t)(X.hptr[g.side][(size_t)g.e] + g.start + (int64_t)t * kGsSub));
     }
     cur += nsb;
-    if (cur >= kGsTarget) close_wave();
+    if (cur >= kGsTarget || ++nseg >= kGsMaxSeg) close_wave();
   }
   if (cur > 0) close_wave();
   const int64_t nd = (int64_t)desc.size();
