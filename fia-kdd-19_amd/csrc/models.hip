@@ -1281,145 +1281,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRowsWaves))
 }
 
 // ------------------------------------------------------------------------------------
-// MF, k = 16 (the headline): 16 lanes per side system, 4 systems (2 queries) per wave.  Lane t
-// owns row t of the side block H = (2/n) Gram + wd I_k + damping I (coordinates 0..15 the
-// embedding, 16 the bias, eliminated last): a[c] = H[t][c] for c <= t, hb = H[16][t], and the
-// right-hand side y_t = v_t (v = [the other side's embedding ; 1], gnn:155 / mf:194).  A
-// right-looking LDL^T: step J broadcasts the pivot column from its owners by DPP
-// row_newbcast (one 16-lane DPP row = one system, no LDS), every lane updates its row, its
-// bias entry and its rhs; the bias pivot comes last.  Back solve by 16-lane DPP row sums.
-// Replaces the thread-per-system k_solve_tps at k = 16 (one lane held a whole 17x17 block in
-// 256 VGPRs: 378 waves for 12 k queries, one per SIMD, every dependent step exposed).
-// ------------------------------------------------------------------------------------
-// a[c] -= l H[c][J] for c = C .. 15, H[c][J] = lane c's a[J] (before this step scales it)
-template <int J, int C>
-__device__ __forceinline__ void mf16_update(double (&a)[16], double l) {
-  if constexpr (C < 16) {
-    a[C] = fma(-l, dpp_d<0x150 + C>(a[J]), a[C]);
-    mf16_update<J, C + 1>(a, l);
-  }
-}
-
-template <int J>
-__device__ __forceinline__ void mf16_step(double (&a)[16], double& hb, double& hbb, double& y, double& y16,
-                                          double& dinv, double& lbt, int t) {
-  const double dj = dpp_d<0x150 + J>(a[J]);          // H[J][J] from lane J
-  double ij = __builtin_amdgcn_rcp(dj);
-  ij = fma(ij, fma(-dj, ij, 1.0), ij);
-  ij = fma(ij, fma(-dj, ij, 1.0), ij);
-  const double yj = dpp_d<0x150 + J>(y), hj = dpp_d<0x150 + J>(hb);
-  const double l = t > J ? a[J] * ij : 0.0;          // L[t][J]
-  const double lb = hj * ij;                         // L[16][J]
-  mf16_update<J, J + 1>(a, l);                      // H[t][c] -= L[t][J] H[c][J]
-  hb = t > J ? fma(-lb, a[J], hb) : hb;              // H[16][t] -= L[16][J] H[t][J]
-  hbb = fma(-lb, hj, hbb);
-  y = fma(-l, yj, y);
-  y16 = fma(-lb, yj, y16);
-  if (t == J) {
-    dinv = ij;
-    lbt = lb;
-  }
-  a[J] = l;
-}
-
-template <int J>
-__device__ __forceinline__ void mf16_steps(double (&a)[16], double& hb, double& hbb, double& y, double& y16,
-                                           double& dinv, double& lbt, int t) {
-  if constexpr (J < 16) {
-    mf16_step<J>(a, hb, hbb, y, y16, dinv, lbt, t);
-    mf16_steps<J + 1>(a, hb, hbb, y, y16, dinv, lbt, t);
-  }
-}
-
-template <class M>
-__global__ __launch_bounds__(64) void k_solve_mf16(QueryArgs A, int64_t Q, double* __restrict__ rec,
-                                                   double* __restrict__ x_out, int32_t* __restrict__ coupled) {
-  static_assert(!M::ncf && M::K == 16, "MF k = 16");
-  constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
-  const int lane = threadIdx.x, sys = lane >> 4, t = lane & 15, h = sys >> 1, sd = sys & 1;
-  const int64_t q = (int64_t)blockIdx.x * 2 + h;
-  const bool active = q < Q;
-  const int64_t qc = active ? q : Q - 1;
-  int32_t u = A.qu[qc], i = A.qi[qc];
-  const bool okid = u >= 0 && u < A.U && i >= 0 && i < A.I;
-  if (!okid) u = i = 0;
-  const int32_t ent = sd ? i : u, oth = sd ? u : i;
-  // the block's raw loads first (row t of the packed triangle, the bias row entry and
-  // diagonal, the rhs), then the list lengths and the pair probe
-  const double* __restrict__ G = A.gram[sd] + (int64_t)ent * GSP;
-  const double* __restrict__ Gr = G + (t * (t + 1)) / 2;
-  double a[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) a[c] = Gr[c <= t ? c : t];
-  double hb = G[tri(K, t)], hbb = G[tri(K, K)];
-  const double vt = (double)A.t[sd ? 0 : 1][(int64_t)oth * K + t];
-  const int64_t n = okid ? (A.ptr[0][u + 1] - A.ptr[0][u]) + (A.ptr[1][i + 1] - A.ptr[1][i]) : 0;
-  double cdup = 0.0, rsum = 0.0;
-  if (n > 0) A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
-  const double s2n = n > 0 ? 2.0 / (double)n : 0.0;
-#pragma unroll
-  for (int c = 0; c < 16; ++c) a[c] = c <= t ? a[c] * s2n + (c == t ? A.wd + A.damping : 0.0) : 0.0;
-  hb *= s2n;
-  hbb = fma(hbb, s2n, A.damping);
-  double y = vt, y16 = 1.0, dinv = 0.0, lbt = 0.0;
-  mf16_steps<0>(a, hb, hbb, y, y16, dinv, lbt, t);
-  double i16 = __builtin_amdgcn_rcp(hbb);
-  i16 = fma(i16, fma(-hbb, i16, 1.0), i16);
-  i16 = fma(i16, fma(-hbb, i16, 1.0), i16);
-  const double zt = y * dinv, x16 = y16 * i16;
-  // L^T x = z: x_r = z_r - sum_{c > r} L[c][r] x_c - L[16][r] x_16, the sum over the system's lanes
-  double xt = 0.0;
-#pragma unroll
-  for (int r = 15; r >= 0; --r) {
-    const double sr = row_sum16(t > r ? a[r] * xt : 0.0);
-    if (t == r) xt = zt - sr - lbt * x16;
-  }
-  // record pieces: theta block, x.v, wd x.theta, r-hat(u,i) (sums over the query's two systems)
-  const double th = (double)A.t[sd][(int64_t)ent * K + t];
-  const double bself = (double)A.t[2 + sd][ent];
-  const double gb = (double)A.t[4][0];
-  const double cq = sys_sum<16>(xt * th) * A.wd;
-  const double xg = sys_sum<16>(fma(xt, vt, t == 0 ? x16 : 0.0));
-  const double pv = row_sum16(th * vt);
-  const double bpair = sys_sum<16>(t == 0 ? bself : 0.0);
-  if (!active) return;
-  if (n == 0) {
-    if (x_out) {
-      x_out[q * D + M::ref_index(sd * Ds + t)] = NAN;
-      if (t == 0) x_out[q * D + M::ref_index(sd * Ds + K)] = NAN;
-    }
-    if (sd == 0 && t == 0) rec[q * M::R] = NAN;
-    return;
-  }
-  if (cdup > 0.0) {               // the test pair is a train row: the full-D k_solve finishes it
-    if (sd == 0 && t == 0) {
-      const int slot = atomicAdd(coupled, 1);
-      coupled[1 + slot] = (int32_t)q;
-    }
-    return;
-  }
-  double* __restrict__ R = rec + q * M::R;
-  if (sd == 0 && t == 0) {
-    R[0] = 1.0 / (double)n;
-    R[1] = cq;
-    R[2] = xg;
-    R[3] = pv + bpair + gb;        // r-hat(u,i)
-  }
-  double* __restrict__ S = R + 4 + sd * M::SB;
-  S[t] = th;
-  S[K + t] = xt;
-  if (t == 0) {
-    S[2 * K] = bself + gb;
-    S[2 * K + 1] = x16;
-    S[2 * K + 2] = (double)oth;
-  }
-  if (x_out) {
-    x_out[q * D + M::ref_index(sd * Ds + t)] = xt;
-    if (t == 0) x_out[q * D + M::ref_index(sd * Ds + K)] = x16;
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // MF, k <= 16: thread-per-system solve.  Every lane owns one (query, side) block of
 // H_t (user block for even lanes, item block for odd lanes) and factors it with
 // LDL^T entirely in registers (153 doubles at k=16, fully unrolled), then solves.  A
@@ -2850,20 +2711,15 @@ QueryArgs make_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
   return A;
 }
 
-// MF k = 16: 16 lanes per side system (k_solve_mf16); MF k = 8: a thread per system
-template <class M>
-constexpr bool use_solve16() {
-  return !M::ncf && M::K == 16;
-}
 template <class M>
 constexpr bool use_tps() {
-  return !M::ncf && M::Ds <= 17 && !use_solve16<M>();
+  return !M::ncf && M::Ds <= 17;
 }
 
 // side systems on 16x16 tiles: NCF (Ds = 2k) and MF k >= 32 (k coordinates + the bias)
 template <class M>
 constexpr bool use_tile_solve() {
-  return !use_tps<M>() && !use_solve16<M>() && (M::ncf ? M::Ds : M::K) % 16 == 0 && (M::ncf ? M::Ds : M::K) <= 64;
+  return !use_tps<M>() && (M::ncf ? M::Ds : M::K) % 16 == 0 && (M::ncf ? M::Ds : M::K) <= 64;
 }
 
 // NCF k <= 16: both side blocks in one wave, a column per lane (k_solve_col)
@@ -2876,7 +2732,7 @@ constexpr bool use_col_solve() {
 // k_solve_col, MF k in {32, 64} and NCF k = 32 k_solve_tile
 template <class M>
 constexpr bool solve_covered() {
-  return use_solve16<M>() || use_tps<M>() || pair_layout<M>() || use_col_solve<M>() || use_tile_solve<M>();
+  return use_tps<M>() || pair_layout<M>() || use_col_solve<M>() || use_tile_solve<M>();
 }
 
 // MF k <= 16 item runs: slice cost target (descriptor cost units per one-wave slice; ml-1m-ex
@@ -3071,10 +2927,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
   if (Q > 0 && !x_in) {
-    if constexpr (use_solve16<M>()) {
-      hipLaunchKernelGGL(k_solve_mf16<M>, dim3((unsigned)((Q + 1) / 2)), dim3(64), 0, s, A, Q, c->rec.as<double>(),
-                         x_out, c->coupled.as<int32_t>());
-    } else if constexpr (use_tps<M>()) {
+    if constexpr (use_tps<M>()) {
       hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                          c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else if constexpr (pair_layout<M>()) {
