@@ -41,6 +41,8 @@ __device__ __forceinline__ d4_t mfma4(double a, double b, d4_t c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+typedef __attribute__((address_space(3))) void* lds_vp;         // LDS-DMA destination
+typedef const __attribute__((address_space(1))) void* glb_vp;   // ... and its global source
 
 __device__ __forceinline__ double wsum(double x) {
 #pragma unroll

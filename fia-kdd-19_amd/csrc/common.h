@@ -12,10 +12,6 @@
 
 namespace fia {
 
-// LDS-DMA (global_load_lds_dwordx4) pointer types
-typedef __attribute__((address_space(3))) void* lds_vp;         // LDS-DMA destination
-typedef const __attribute__((address_space(1))) void* glb_vp;   // ... and its global source
-
 constexpr int kWave = 64;
 constexpr int kScoreThreads = 256;       // scoring workgroup (4 independent waves)
 constexpr int kScoreRows = 4;            // related ratings per lane and chunk

@@ -1312,22 +1312,12 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
   const float* Eself = side == 0 ? A.t[0] : A.t[1];
   const float* Eoth = side == 0 ? A.t[1] : A.t[0];
   const float* Bself = side == 0 ? A.t[2] : A.t[3];
-  // The wave's 64 cached blocks go to LDS first, by coalesced DMA (global_load_lds_dwordx4, 1 KB
-  // per instruction, the blocks back to back): a lane loading its own block directly touched 64
-  // different lines per instruction and the solve waited on the CU's miss queue.  They overlap
-  // the pair lookup's probe chain.
-  constexpr int NB = 64 * GSP * 8 / 1024;
-  static_assert(64 * GSP * 8 % 1024 == 0, "whole 1-KB DMA pieces");
-  __shared__ __attribute__((aligned(16))) double sg[64 * GSP];
-#pragma unroll 4
-  for (int b = 0; b < NB; ++b) {
-    const int byte = 1024 * b + 16 * lane, s = byte / (GSP * 8);
-    const int32_t es = __shfl(ent, s);
-    const double* src = A.gram[s & 1] + (int64_t)es * GSP + (byte - s * GSP * 8) / 8;
-    __builtin_amdgcn_global_load_lds((glb_vp)src, (lds_vp)(sg + 128 * b), 16, 0, 0);
-  }
+  // the cached block's loads go out first: they overlap the pair lookup's probe chain
+  const double* G = A.gram[side] + (int64_t)ent * GSP;
   double h[GS];
 #define HS(t) h[(t)]
+#pragma unroll
+  for (int t = 0; t < GS; ++t) HS(t) = G[t];
   double cdup = 0.0, rsum = 0.0;
   if (active && n > 0)
     A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
@@ -1341,13 +1331,6 @@ __global__ __launch_bounds__(64) void k_solve_tps(QueryArgs A, int64_t Q, double
     if (side == 0) rec[q * M::R] = NAN;
   }
   const bool work = active && n > 0 && cdup == 0.0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the DMA pieces have landed
-  __builtin_amdgcn_wave_barrier();
-  {
-    const double* __restrict__ mine = sg + lane * GSP;   // stride 1232 B: conflict-free b128 reads
-#pragma unroll
-    for (int t = 0; t < GS; ++t) HS(t) = mine[t];
-  }
 
   // H block = (2/n) Gram + wd on the embedding coordinates + damping, in registers (fully
   // unrolled, every index constant)
