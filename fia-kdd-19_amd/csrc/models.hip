@@ -1281,6 +1281,213 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRowsWaves))
 }
 
 // ------------------------------------------------------------------------------------
+// MF, k = 16 (the headline): a quad of lanes per side system, 16 systems (8 queries) per wave.
+// Lane j of a quad owns rows j, j + 4, j + 8, j + 12 of the block's embedding coordinates
+// (slot s = row 4 s + j: a[s][c] = H[r][c] for c <= r), their bias-row entries hb[s] =
+// H[16][r] and right-hand sides y[s] = v_r; the bias pivot H[16][16] (and y_16) is kept by
+// every lane of the quad and eliminated last.  Right-looking LDL^T: step J broadcasts the
+// pivot column inside the quad by DPP quad_perm (no LDS), every lane updates its rows; the
+// back solve sums each row's terms by two quad DPP steps.  A thread per system (k_solve_tps,
+// k = 8) held the whole 17 x 17 block in one lane: at k = 16 that was 256 VGPRs with AGPR
+// spills, 378 waves for 12 k queries (one per SIMD), every dependent step exposed.
+// ------------------------------------------------------------------------------------
+// every lane of the quad gets lane L's value (DPP quad_perm [L, L, L, L])
+template <int L>
+__device__ __forceinline__ double quad_bcast(double x) {
+  return dpp_d<(L | (L << 2) | (L << 4) | (L << 6))>(x);
+}
+__device__ __forceinline__ double quad_sum(double x) {
+  x += dpp_d<0xB1>(x);      // quad_perm [1, 0, 3, 2]
+  x += dpp_d<0x4E>(x);      // quad_perm [2, 3, 0, 1]
+  return x;
+}
+
+struct Quad16 {
+  double a[4][16];          // slot s: row 4 s + j, columns 0 .. 4 s + 3 (past the row: unused)
+  double hb[4], y[4], dinv[4], lbt[4], x[4];
+  double hbb, y16;
+};
+
+// column J entries H[c][J], c = C .. 15, from lane c % 4 (slot c / 4), before step J scales them
+template <int J, int C>
+__device__ __forceinline__ void quad_col(const Quad16& Z, double (&hc)[16]) {
+  if constexpr (C < 16) {
+    hc[C] = quad_bcast<C % 4>(Z.a[C / 4][J]);
+    quad_col<J, C + 1>(Z, hc);
+  }
+}
+
+template <int J, int S>
+__device__ __forceinline__ void quad_rows(Quad16& Z, const double (&hc)[16], double ij, double lb, double yj, int j) {
+  if constexpr (S < 4) {
+    // slot S holds row r = 4 S + j: below the pivot for S > J / 4, for S == J / 4 iff j > J % 4
+    const bool below = S > J / 4 || (S == J / 4 && j > J % 4);
+    const double l = below ? Z.a[S][J] * ij : 0.0;          // L[r][J]
+#pragma unroll
+    for (int c = J + 1; c < 4 * S + 4; ++c) Z.a[S][c] = fma(-l, hc[c], Z.a[S][c]);
+    Z.hb[S] = below ? fma(-lb, Z.a[S][J], Z.hb[S]) : Z.hb[S];   // H[16][r] -= L[16][J] H[r][J]
+    Z.y[S] = fma(-l, yj, Z.y[S]);
+    if (below) Z.a[S][J] = l;
+    quad_rows<J, S + 1>(Z, hc, ij, lb, yj, j);
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void quad_steps(Quad16& Z, int j) {
+  if constexpr (J < 16) {
+    constexpr int SJ = J / 4, JJ = J % 4;
+    const double dj = quad_bcast<JJ>(Z.a[SJ][J]);
+    double ij = __builtin_amdgcn_rcp(dj);
+    ij = fma(ij, fma(-dj, ij, 1.0), ij);
+    ij = fma(ij, fma(-dj, ij, 1.0), ij);
+    const double yj = quad_bcast<JJ>(Z.y[SJ]), hj = quad_bcast<JJ>(Z.hb[SJ]);
+    const double lb = hj * ij;                              // L[16][J]
+    double hc[16];
+    quad_col<J, J + 1>(Z, hc);
+    quad_rows<J, SJ>(Z, hc, ij, lb, yj, j);
+    Z.hbb = fma(-lb, hj, Z.hbb);
+    Z.y16 = fma(-lb, yj, Z.y16);
+    if (j == JJ) {
+      Z.dinv[SJ] = ij;
+      Z.lbt[SJ] = lb;
+    }
+    quad_steps<J + 1>(Z, j);
+  }
+}
+
+// L^T x = z from row 15 down: x_r = z_r - sum_{c > r} L[c][r] x_c - L[16][r] x_16
+template <int R>
+__device__ __forceinline__ void quad_back(Quad16& Z, const double (&z)[4], double x16, int j) {
+  if constexpr (R >= 0) {
+    constexpr int SR = R / 4, JR = R % 4;
+    double p = 0.0;
+#pragma unroll
+    for (int s = SR; s < 4; ++s) {
+      const bool below = s > SR || j > JR;                 // row 4 s + j > R
+      p = below ? fma(Z.a[s][R], Z.x[s], p) : p;
+    }
+    p = quad_sum(p);
+    if (j == JR) Z.x[SR] = z[SR] - p - Z.lbt[SR] * x16;
+    quad_back<R - 1>(Z, z, x16, j);
+  }
+}
+
+template <class M>
+__global__ __launch_bounds__(64) void k_solve_quad(QueryArgs A, int64_t Q, double* __restrict__ rec,
+                                                   double* __restrict__ x_out, int32_t* __restrict__ coupled) {
+  static_assert(!M::ncf && M::K == 16, "MF k = 16");
+  constexpr int K = M::K, Ds = M::Ds, D = M::D, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
+  const int lane = threadIdx.x, qd = lane >> 2, j = lane & 3, h = qd >> 1, sd = qd & 1;
+  const int64_t q = (int64_t)blockIdx.x * 8 + h;
+  const bool active = q < Q;
+  const int64_t qc = active ? q : Q - 1;
+  int32_t u = A.qu[qc], i = A.qi[qc];
+  const bool okid = u >= 0 && u < A.U && i >= 0 && i < A.I;
+  if (!okid) u = i = 0;
+  const int32_t ent = sd ? i : u, oth = sd ? u : i;
+  // the block's loads first (rows 4 s + j of the packed triangle, their bias-row entries, the
+  // bias diagonal, the rhs), then the list lengths and the pair probe
+  const double* __restrict__ G = A.gram[sd] + (int64_t)ent * GSP;
+  const float* __restrict__ Eo = A.t[sd ? 0 : 1] + (int64_t)oth * K;
+  Quad16 Z;
+  double vv[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int r = 4 * s + j;
+    const double* __restrict__ Gr = G + (r * (r + 1)) / 2;
+#pragma unroll
+    for (int c = 0; c < 4 * s + 4; ++c) Z.a[s][c] = Gr[c <= r ? c : r];
+    Z.hb[s] = G[tri(K, r)];
+    vv[s] = (double)Eo[r];
+  }
+  Z.hbb = G[tri(K, K)];
+  const int64_t n = okid ? (A.ptr[0][u + 1] - A.ptr[0][u]) + (A.ptr[1][i + 1] - A.ptr[1][i]) : 0;
+  double cdup = 0.0, rsum = 0.0;
+  if (n > 0) A.pairs.lookup((unsigned long long)u * (unsigned long long)A.I + (unsigned long long)i, cdup, rsum);
+  // H block = (2/n) Gram + wd on the embedding coordinates + damping
+  const double s2n = n > 0 ? 2.0 / (double)n : 0.0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int r = 4 * s + j;
+#pragma unroll
+    for (int c = 0; c < 4 * s + 4; ++c) Z.a[s][c] = c <= r ? fma(Z.a[s][c], s2n, c == r ? A.wd + A.damping : 0.0) : 0.0;
+    Z.hb[s] *= s2n;
+    Z.y[s] = vv[s];
+    Z.dinv[s] = Z.lbt[s] = Z.x[s] = 0.0;
+  }
+  Z.hbb = fma(Z.hbb, s2n, A.damping);
+  Z.y16 = 1.0;
+  quad_steps<0>(Z, j);
+  double i16 = __builtin_amdgcn_rcp(Z.hbb);
+  i16 = fma(i16, fma(-Z.hbb, i16, 1.0), i16);
+  i16 = fma(i16, fma(-Z.hbb, i16, 1.0), i16);
+  const double x16 = Z.y16 * i16;
+  double z[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) z[s] = Z.y[s] * Z.dinv[s];
+  quad_back<15>(Z, z, x16, j);
+  // record pieces: theta block, x.v, wd x.theta, r-hat(u,i) (sums over the query's two systems:
+  // the quad, then the neighbouring quad)
+  const float* __restrict__ Es = A.t[sd] + (int64_t)ent * K;
+  double th[4], cq = 0.0, xg = j == 0 ? x16 : 0.0, pv = 0.0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    th[s] = (double)Es[4 * s + j];
+    cq = fma(Z.x[s], th[s], cq);
+    xg = fma(Z.x[s], vv[s], xg);
+    pv = fma(th[s], vv[s], pv);
+  }
+  cq = quad_sum(cq);
+  xg = quad_sum(xg);
+  pv = quad_sum(pv);
+  cq = (cq + __shfl_xor(cq, 4)) * A.wd;
+  xg += __shfl_xor(xg, 4);
+  const double bself = (double)A.t[2 + sd][ent];
+  const double gb = (double)A.t[4][0];
+  const double bpair = bself + __shfl_xor(bself, 4);
+  if (!active) return;
+  if (n == 0) {
+    if (x_out) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) x_out[q * D + M::ref_index(sd * Ds + 4 * s + j)] = NAN;
+      if (j == 0) x_out[q * D + M::ref_index(sd * Ds + K)] = NAN;
+    }
+    if (sd == 0 && j == 0) rec[q * M::R] = NAN;
+    return;
+  }
+  if (cdup > 0.0) {               // the test pair is a train row: the full-D k_solve finishes it
+    if (sd == 0 && j == 0) {
+      const int slot = atomicAdd(coupled, 1);
+      coupled[1 + slot] = (int32_t)q;
+    }
+    return;
+  }
+  double* __restrict__ R = rec + q * M::R;
+  if (sd == 0 && j == 0) {
+    R[0] = 1.0 / (double)n;
+    R[1] = cq;
+    R[2] = xg;
+    R[3] = pv + bpair + gb;        // r-hat(u,i)
+  }
+  double* __restrict__ S = R + 4 + sd * M::SB;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    S[4 * s + j] = th[s];
+    S[K + 4 * s + j] = Z.x[s];
+  }
+  if (j == 0) {
+    S[2 * K] = bself + gb;
+    S[2 * K + 1] = x16;
+    S[2 * K + 2] = (double)oth;
+  }
+  if (x_out) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) x_out[q * D + M::ref_index(sd * Ds + 4 * s + j)] = Z.x[s];
+    if (j == 0) x_out[q * D + M::ref_index(sd * Ds + K)] = x16;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // MF, k <= 16: thread-per-system solve.  Every lane owns one (query, side) block of
 // H_t (user block for even lanes, item block for odd lanes) and factors it with
 // LDL^T entirely in registers (153 doubles at k=16, fully unrolled), then solves.  A
@@ -2711,15 +2918,21 @@ QueryArgs make_args(fia_ctx* c, const int32_t* qu, const int32_t* qi) {
   return A;
 }
 
+// MF k = 16: a quad of lanes per side system (k_solve_quad); MF k = 8: a thread per system
+template <class M>
+constexpr bool use_quad_solve() {
+  return !M::ncf && M::K == 16;
+}
 template <class M>
 constexpr bool use_tps() {
-  return !M::ncf && M::Ds <= 17;
+  return !M::ncf && M::Ds <= 17 && !use_quad_solve<M>();
 }
 
 // side systems on 16x16 tiles: NCF (Ds = 2k) and MF k >= 32 (k coordinates + the bias)
 template <class M>
 constexpr bool use_tile_solve() {
-  return !use_tps<M>() && (M::ncf ? M::Ds : M::K) % 16 == 0 && (M::ncf ? M::Ds : M::K) <= 64;
+  return !use_tps<M>() && !use_quad_solve<M>() && (M::ncf ? M::Ds : M::K) % 16 == 0 &&
+         (M::ncf ? M::Ds : M::K) <= 64;
 }
 
 // NCF k <= 16: both side blocks in one wave, a column per lane (k_solve_col)
@@ -2732,7 +2945,7 @@ constexpr bool use_col_solve() {
 // k_solve_col, MF k in {32, 64} and NCF k = 32 k_solve_tile
 template <class M>
 constexpr bool solve_covered() {
-  return use_tps<M>() || pair_layout<M>() || use_col_solve<M>() || use_tile_solve<M>();
+  return use_quad_solve<M>() || use_tps<M>() || pair_layout<M>() || use_col_solve<M>() || use_tile_solve<M>();
 }
 
 // MF k <= 16 item runs: slice cost target (descriptor cost units per one-wave slice; ml-1m-ex
@@ -2927,7 +3140,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   }
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
   if (Q > 0 && !x_in) {
-    if constexpr (use_tps<M>()) {
+    if constexpr (use_quad_solve<M>()) {
+      hipLaunchKernelGGL(k_solve_quad<M>, dim3((unsigned)((Q + 7) / 8)), dim3(64), 0, s, A, Q, c->rec.as<double>(),
+                         x_out, c->coupled.as<int32_t>());
+    } else if constexpr (use_tps<M>()) {
       hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                          c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else if constexpr (pair_layout<M>()) {
