@@ -209,7 +209,7 @@ int fia_destroy(fia_ctx* c) {
                              &c->gpart[s], &c->self[s], &c->gm[s], &c->slot[s], &c->bitems[s], &c->bcomb[s]})
         rel(*b);
     }
-    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->cand_row, &c->qscan,
+    fia::DevBuf* bufs[] = {&c->rec,    &c->coff,   &c->cdesc,    &c->cand_pos,  &c->cand_val, &c->qscan,
                            &c->flag,   &c->nch,    &c->coupled,  &c->idx.pkey,  &c->idx.pcnt, &c->idx.psum,
                            &c->gcnt,   &c->gstart, &c->grank,    &c->gq,        &c->qbase,    &c->gscan,
                            &c->wstart, &c->witems, &c->resid,  &c->qwork,  &c->xb,       &c->syslist,

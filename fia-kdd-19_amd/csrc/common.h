@@ -208,7 +208,6 @@ struct fia_ctx {
   fia::DevBuf cdesc;      // ChunkDesc [max chunks]
   fia::DevBuf cand_pos;   // int32 [max chunks * K]
   fia::DevBuf cand_val;   // double [max chunks * K]
-  fia::DevBuf cand_row;   // int32 [max chunks]: train row of a chunk's top-1 (MF k <= 16, K = 1)
   fia::DevBuf qscan;      // k_query_scan tile words + counters (left zero by every launch)
   fia::DevBuf flag;       // int32 [4] device status words
   fia::DevBuf nch;        // int64 [Q+1] chunk counts
@@ -347,12 +346,11 @@ hipError_t launch_gram_mf_stream(int k, const GramStreamArgs& G, hipStream_t s);
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t Q,
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
-                                double* cand_val, int32_t* cand_row, PhaseSpan ps);
+                                double* cand_val, PhaseSpan ps);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
-// cand_row (K = 1, optional): the candidates' train rows, written by the scoring kernel
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
-                             int64_t max_chunks, const int32_t* cand_row = nullptr);
+                             int64_t max_chunks);
 
 // phase event helpers (no-ops unless profiling)
 void phase_begin(fia_ctx* c, int phase, hipStream_t s);

@@ -2846,29 +2846,10 @@ __global__ __launch_bounds__(256) void k_topk_merge_thread(
     int K, int spc, const int32_t* __restrict__ cand_pos, const double* __restrict__ cand_val,
     const int64_t* __restrict__ uptr, const int32_t* __restrict__ urow, const int64_t* __restrict__ iptr,
     const int32_t* __restrict__ irow, int64_t U, int64_t I, int64_t* __restrict__ topk_pos,
-    int64_t* __restrict__ topk_idx, double* __restrict__ topk_val, const int32_t* __restrict__ cand_row) {
+    int64_t* __restrict__ topk_idx, double* __restrict__ topk_val) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Q) return;
   const int64_t cb = coff[q] * spc * K, ce = coff[q + 1] * spc * K;
-  if (cand_row) {
-    // K = 1 with the candidates' train rows from the scoring kernel: one dependent round trip
-    // (the chunk offsets, then every slot's three words), no list lookup
-    double ba = -2.0, bv = 0.0;
-    int bp = 0x7fffffff;
-    int32_t br = -1;
-    for (int64_t c = cb; c < ce; ++c) {
-      const int p = cand_pos[c];
-      const double vv = cand_val[c];
-      const int32_t rw = cand_row[c];
-      const double a = topk_key(vv);
-      if (p >= 0 && better(a, p, ba, bp)) { ba = a; bp = p; bv = vv; br = rw; }
-    }
-    const bool ok = ba > -1.5;
-    topk_pos[q] = ok ? bp : -1;
-    topk_idx[q] = ok ? (int64_t)br : -1;
-    topk_val[q] = ok ? bv : NAN;
-    return;
-  }
   const int32_t u = qu[q], i = qi[q];
   const bool ok_id = (u >= 0 && u < U && i >= 0 && i < I);
   const int64_t ub = ok_id ? uptr[u] : 0, du = ok_id ? uptr[u + 1] - ub : 0, ib = ok_id ? iptr[i] : 0;
@@ -3108,7 +3089,6 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   if (K > 0) {
     FIA_HIP_TRY(c->cand_pos.reserve(sizeof(int32_t) * (size_t)((max_chunks + 1) * K * spc), s));
     FIA_HIP_TRY(c->cand_val.reserve(sizeof(double) * (size_t)((max_chunks + 1) * K * spc), s));
-    if (runs && K == 1) FIA_HIP_TRY(c->cand_row.reserve(sizeof(int32_t) * (size_t)(max_chunks + 1), s));
   }
   QueryArgs A = make_args(c, qu, qi);
   const int64_t nE = c->idx.U + c->idx.I;
@@ -3236,15 +3216,13 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     if constexpr (runs)
       FIA_HIP_TRY(launch_score_mf_runs(M::K, grid, s, A, Q, c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
                                        c->slices.as<int32_t>(), c->rec.as<double>(), rel_idx, influence, K,
-                                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>(),
-                                       c->cand_row.as<int32_t>(), span));
+                                       c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), span));
   }
   FIA_HIP_TRY(hipGetLastError());
 topk:
   if (K > 0 && Q > 0) {
     phase_begin(c, 3, s);
-    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, spc, topk_pos, topk_idx, topk_val, s, max_chunks,
-                                  runs && K == 1 ? c->cand_row.as<int32_t>() : nullptr));
+    FIA_HIP_TRY(launch_topk_merge(c, Q, qu, qi, K, spc, topk_pos, topk_idx, topk_val, s, max_chunks));
     phase_end(c, 3, s);
   }
   return hipSuccess;
@@ -3266,7 +3244,7 @@ bool model_supported(int model, int k) {
 
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
-                             int64_t max_chunks, const int32_t* cand_row) {
+                             int64_t max_chunks) {
   if (K <= 0 || Q <= 0) return hipSuccess;
   // a thread per query while the queries have few chunks (<= 16 on average: ml-1m-ex,
   // yelp-ex); a wave per query over long candidate lists (20M: ~170 chunks per query)
@@ -3275,7 +3253,7 @@ hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int
                        c->coff.as<int64_t>(), K, spc, c->cand_pos.as<int32_t>(), c->cand_val.as<double>(),
                        c->idx.side[0].ptr.as<int64_t>(), c->idx.side[0].row.as<int32_t>(),
                        c->idx.side[1].ptr.as<int64_t>(), c->idx.side[1].row.as<int32_t>(), c->p.U, c->p.I, topk_pos,
-                       topk_idx, topk_val, K == 1 ? cand_row : nullptr);
+                       topk_idx, topk_val);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_topk_merge, dim3((unsigned)Q), dim3(64), 0, s, qu, qi, Q, c->coff.as<int64_t>(), K, spc,

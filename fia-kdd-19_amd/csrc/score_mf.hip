@@ -134,8 +134,7 @@ template <class M, int KM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))) void k_score_mf_runs(
     RunArgs A, int64_t Q, const ChunkDesc* __restrict__ cdesc, const int64_t* __restrict__ qbase,
     const int32_t* __restrict__ slices, const double* __restrict__ rec, int32_t* __restrict__ rel_idx,
-    double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val,
-    int32_t* __restrict__ cand_row) {
+    double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
   static_assert(!M::ncf && M::K <= 16 && M::K % 4 == 0, "MF k in {8, 16}");
   constexpr int K = M::K, RT = kRunChunk / 64, NA = K / 4;
   const int lane = threadIdx.x & 63;
@@ -330,14 +329,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
           const bool okk = ba > -1.5;
           const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(cand_pos + slot, 0, 4, kBufWord3);
           const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(cand_val + slot, 0, 8, kBufWord3);
-          const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(cand_row + slot, 0, 4, kBufWord3);
           const long long vb = __double_as_longlong(okk ? bv : (double)NAN);
-          // the winner's train row (its lane's list entry): the merge needs no list lookup
-          int32_t wr = row[0];
-#pragma unroll
-          for (int r = 1; r < RT; ++r) wr = (bp >> 6) == r ? row[r] : wr;
-          wr = __builtin_amdgcn_readlane(wr, bp & 63);
-          __builtin_amdgcn_raw_buffer_store_b32((unsigned)(okk ? wr : -1), rw, lane * 4, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b32((unsigned)(okk ? pbj + co + bp : -1), rp, lane * 4, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(
               (__attribute__((ext_vector_type(2))) unsigned){(unsigned)(vb & 0xffffffffll), (unsigned)(vb >> 32)}, rv,
@@ -387,7 +379,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& QA, int64_t Q,
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
-                                double* cand_val, int32_t* cand_row, PhaseSpan ps) {
+                                double* cand_val, PhaseSpan ps) {
   RunArgs A{};
   for (int sd = 0; sd < 2; ++sd) {
     A.other[sd] = QA.other[sd];
@@ -399,7 +391,7 @@ hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryA
 #define FIA_RUNS_LAUNCH(KK, KM)                                                                                      \
   hipExtLaunchKernelGGL((k_score_mf_runs<MFm<KK>, KM>), dim3((unsigned)grid), dim3(64), 0, s, ps.a, ps.b, 0, A, Q, \
                         cdesc,                                                                                    \
-                     qbase, slices, rec, rel_idx, influence, K, cand_pos, cand_val, cand_row)
+                     qbase, slices, rec, rel_idx, influence, K, cand_pos, cand_val)
   const int km = K <= 0 ? 0 : K == 1 ? 1 : 2;
   if (k == 16) {
     if (km == 0) FIA_RUNS_LAUNCH(16, 0); else if (km == 1) FIA_RUNS_LAUNCH(16, 1); else FIA_RUNS_LAUNCH(16, 2);
