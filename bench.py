@@ -102,6 +102,10 @@ def parse(argv=None):
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="auto: nccl (RCCL) when every rank has a GPU of its own, gloo when ranks share one")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--rq2", action="store_true",
+                    help="RQ2 single-query latency instead of the throughput line: ml-1m-ex test_idx 59 and "
+                         "yelp-ex test_idx 1, MF and NCF k=16 (reference src/scripts/RQ2.py:53,57), GPU through "
+                         "the facade beside the reference algorithm's CPU time for the same query")
     return ap.parse_args(argv)
 
 
@@ -389,8 +393,58 @@ def compulsory_bytes(cfg, qu, qi, deg_u, deg_i, bounds):
     return tot / max(len(bounds) - 1, 1)
 
 
+def rq2_main(args):
+    """RQ2 (reference src/scripts/RQ2.py, experiments.record_time_cost): the latency of ONE
+    query -- ml-1m-ex test_idx 59, yelp-ex test_idx 1, MF and NCF k=16 -- as the reference times
+    it (get_influence_on_test_loss: related set, inverse HVP, per-rating influence), GPU through
+    the facade (fia-kdd-19_amd/scripts/RQ2.py: median of 5 calls after a warm-up; the three stage
+    timers from the call's HIP events and the call's host wall time), beside the reference
+    ALGORITHM on this host's CPU for the same query (oracle/ncg_port.py: np.where scans + scipy
+    fmin_ncg with the reference arguments + the per-rating gradient loop; one process, BLAS
+    threads = the usable cores; median of 3).  The CPU runs first, before the GPU is touched."""
+    from influence import synth
+    from oracle import ncg_port
+    cases = []
+    for data, test_idx in (("ml1m", 59), ("yelp", 1)):
+        d = synth.make_dataset(synth.ML1M if data == "ml1m" else synth.YELP, seed=0)
+        tu, ti, tr = d["train"]
+        u, i = int(d["test"][0][test_idx]), int(d["test"][1][test_idx])
+        for model in ("MF", "NCF"):
+            params = (synth.mf_params if model == "MF" else synth.ncf_params)(d["U"], d["I"], 16, 0)
+            ref = ncg_port.RefAlgorithm(model, params, 16, tu, ti, tr, 1e-3, 1e-6)
+            from threadpoolctl import threadpool_limits
+            ts = []
+            with threadpool_limits(cpu_cores()):
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    ref.get_influence_on_test_loss(u, i)
+                    ts.append(time.perf_counter() - t0)
+            cases.append(dict(dataset="ml-1m-ex" if data == "ml1m" else "yelp-ex", model=model, test_idx=test_idx,
+                              user=u, item=i, cpu_reference_algorithm_s=float(np.median(ts)), cpu_cores=cpu_cores()))
+    import torch
+    torch.cuda.set_device(0)
+    from scripts import RQ2
+    from scripts.load_movielens import load_movielens_synthetic
+    from scripts.load_yelp import load_yelp_synthetic
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="rq2_")
+    cfg = dict(RQ2.configs)
+    for c in cases:
+        ds = load_movielens_synthetic(0) if c["dataset"] == "ml-1m-ex" else load_yelp_synthetic(0)
+        m = RQ2.build("movielens" if c["dataset"] == "ml-1m-ex" else "yelp", c["model"], cfg, ds, train_dir=tmp)
+        g = RQ2.time_query(m, c["test_idx"], cfg["repeat"])
+        m.ctx.close()
+        c.update(n_related=g["n"], gpu_inverse_hvp_s=g["inverse_hvp_s"], gpu_multiply_s=g["multiply_s"],
+                 gpu_total_s=g["total_s"], gpu_wall_s=g["wall_s"],
+                 speedup_wall=c["cpu_reference_algorithm_s"] / g["wall_s"])
+    print(json.dumps({"metric": "RQ2 single-query latency (seconds), reference src/scripts/RQ2.py",
+                      "higher_is_better": False, "cpu": cpu_model(), "cases": cases}), flush=True)
+
+
 def main():
     args = parse()
+    if args.rq2:
+        return rq2_main(args)
     rc = launch_ranks(args)
     if rc is not None:
         sys.exit(rc)
