@@ -190,7 +190,7 @@ def score_kernel(cfg, K=1):
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_big_score_mfma"
     if model == "NCF":
-        return "k_score_ncf"
+        return "k_score_ncf_runs" if k <= 16 else "k_score_ncf"
     if k <= 16:
         return "k_score_mf_runs"
     if K <= 1:

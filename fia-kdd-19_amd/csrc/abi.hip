@@ -424,8 +424,9 @@ static int query_batch_common(fia_ctx* c, int64_t Q, const int32_t* qu, const in
     // (small k joins the pending Gram pass right before its solve, after the query scans)
     if (fia::big_supported(c->p.model, c->p.k))
       if (hipError_t es = fia::join_prepare(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
-    // chunk descriptors / candidate slots: at most 2 per query + one per kRunChunk ratings
-    const int64_t max_chunks = 2 * Q + total_rel / fia::kRunChunk + 1;
+    // chunk descriptors / candidate slots: at most 2 per query + one per kNcfRunChunk ratings
+    // (the shortest run chunk)
+    const int64_t max_chunks = 2 * Q + total_rel / fia::kNcfRunChunk + 1;
     bool unsup = false;
     hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,
                                     topk_idx, topk_val, as_stream(stream), unsup, x_in);

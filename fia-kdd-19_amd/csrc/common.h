@@ -18,6 +18,7 @@ constexpr int kScoreRows = 4;            // related ratings per lane and chunk
 constexpr int kChunk = 64 * kScoreRows;  // related ratings per scoring chunk (one wave)
 constexpr int kRunQB = 16;               // queries per item-run block (k_score_mf_runs)
 constexpr int kRunChunk = 128;           // related ratings per item-run descriptor (k_score_mf_runs)
+constexpr int kNcfRunChunk = 64;         // ... for NCF k <= 16 (k_score_ncf_runs: one rating per lane)
 constexpr int kRunUserCost = 3;          // scheduling cost of a user-side run descriptor (k_score_mf_runs
                                          // slices): 2 per descriptor + 1 per query of its run
 
@@ -281,7 +282,7 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 // to a power of two)
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word = nullptr,
-                        bool runs = false, int slice_cost = 0);
+                        bool runs = false, int slice_cost = 0, int run_chunk = kRunChunk);
 hipError_t build_gram_lists(fia_ctx* c, int64_t chunk, hipStream_t s);
 // the MF k <= 16 Gram stream of the current index (Index::gs*), rebuilt after build_index
 hipError_t build_gram_stream(fia_ctx* c, int k, hipStream_t s);
@@ -347,6 +348,11 @@ hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryA
                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
                                 double* cand_val, PhaseSpan ps);
+// NCF k <= 16 item-run scoring (score_mf.hip)
+hipError_t launch_score_ncf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& A, int64_t Q,
+                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
+                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
+                                 double* cand_val, PhaseSpan ps);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,

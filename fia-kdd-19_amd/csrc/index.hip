@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
         s_ub[it] = ub; s_du[it] = du; s_ib[it] = ib; s_di[it] = di;
         x = MODE == 0 ? du + di : (du + kChunk - 1) / kChunk + (di + kChunk - 1) / kChunk;
         if (MODE == 1 && runs) {
-          // packed {chunks (candidate slots) << 31 | work descriptors}, chunks of kRunChunk ratings:
+          // packed {chunks (candidate slots) << 31 | work descriptors}, chunks of clen ratings:
           // the item-side chunks are work only for a run head (first query of a run of equal
           // test items, runs cut at multiples of `runs`), which scores them for the whole run
           const int tt = threadIdx.x;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
             }
             s_nq[it] = nq;
           }
-          const int64_t cu = (du + kRunChunk - 1) / kRunChunk, ci = (di + kRunChunk - 1) / kRunChunk;
+          const int64_t cu = (du + clen - 1) / clen, ci = (di + clen - 1) / clen;
           x = ((cu + ci) << 31) | (cu + (head ? ci : 0));
           tsum2 += cu * kRunUserCost + (head ? ci * (s_nq[it] + 2) : 0);
         }
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
       qbase[4 * q + 0] = s_base[it];
       qbase[4 * q + 1] = s_base[it] + du;
       qbase[4 * q + 2] = cr;
-      qbase[4 * q + 3] = cr + (runs ? (du + kRunChunk - 1) / kRunChunk : (du + kChunk - 1) / kChunk);
+      qbase[4 * q + 3] = cr + (du + clen - 1) / clen;
     }
     if (MODE == 1 && runs) {
       // runs mode: this query's descriptors are written by the whole block below
@@ -340,25 +340,25 @@ __global__ __launch_bounds__(kScanThreads) void k_query_scan(
         const int t = lo;
         const int64_t j = c - f_c0[t];
         const int32_t du = f_du[t], di = f_di[t], nq = f_nq[t];
-        const int64_t cu = (du + kRunChunk - 1) / kRunChunk;
+        const int64_t cu = (du + clen - 1) / clen;
         const int64_t qq = tile * kScanTile + t;
         ChunkDesc d;
         int64_t p, w;
         if (j < cu) {
-          const int64_t st = j * kRunChunk;
+          const int64_t st = j * clen;
           d.list_base = f_ub[t] + st;
           d.out_base = f_base[t] + st;
           d.pos0 = (int32_t)st;
-          d.len = (int32_t)(du - st < kRunChunk ? du - st : kRunChunk);
+          d.len = (int32_t)(du - st < clen ? du - st : clen);
           d.side = 0 | (1 << 8);
           p = f_cost[t] + j * kRunUserCost;
           w = kRunUserCost;
         } else {
-          const int64_t st = (j - cu) * kRunChunk;
+          const int64_t st = (j - cu) * clen;
           d.list_base = f_ib[t] + st;
           d.out_base = f_base[t] + du + st;
           d.pos0 = (int32_t)(du + st);
-          d.len = (int32_t)(di - st < kRunChunk ? di - st : kRunChunk);
+          d.len = (int32_t)(di - st < clen ? di - st : clen);
           d.side = 1 | (nq << 8);
           p = f_cost[t] + cu * kRunUserCost + (j - cu) * (nq + 2);
           w = nq + 2;
@@ -824,7 +824,7 @@ hipError_t write_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t
 
 hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, const int64_t* offsets,
                         int64_t max_chunks, bool offsets_only, hipStream_t s, int32_t* zero_word, bool runs,
-                        int slice_cost) {
+                        int slice_cost, int run_chunk) {
   FIA_HIP_TRY(c->coff.reserve(sizeof(int64_t) * (size_t)(Q + 1), s));
   const bool rq = runs && !offsets_only;
   if (!offsets_only) FIA_HIP_TRY(c->cdesc.reserve(sizeof(ChunkDesc) * (size_t)(max_chunks + 1), s));
@@ -838,7 +838,7 @@ hipError_t build_chunks(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t*
   }
   return launch_query_scan<1>(c, Q, qu, qi, c->coff.as<int64_t>(), offsets,
                               offsets_only ? nullptr : c->cdesc.as<ChunkDesc>(), zero_word, s,
-                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? kRunQB : 0, rq ? kRunChunk : kChunk, lsh,
+                              rq ? c->qbase.as<int64_t>() : nullptr, rq ? kRunQB : 0, rq ? run_chunk : kChunk, lsh,
                               rq ? c->slices.as<int32_t>() : nullptr);
 }
 

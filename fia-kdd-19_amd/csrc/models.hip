@@ -3078,7 +3078,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // runs (k_score_mf_runs, per-query chunks sharing the item's list); MF k in {32, 64}
   // entity-shared, on f64 MFMA for K <= 1 (k_score_mf_mfma, query blocks of 15) and on VALU
   // otherwise (k_score_grouped_mf); NCF entity-shared (k_score_ncf)
-  constexpr bool grouped = M::ncf || M::K >= 32;
+  // item runs: MF k <= 16 (k_score_mf_runs) and NCF k <= 16 (k_score_ncf_runs)
+  constexpr bool grouped = M::ncf ? !mask_path<M>() : M::K >= 32;
   constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);
   const bool use_mfma = mfma_ok && K <= 1;
   const int qblock = use_mfma ? kMfmaQB : query_block<M>();
@@ -3104,7 +3105,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // kRunUserCost per descriptor slot), the surplus waves exit at once
   constexpr int64_t lam = kRunLambda;
   const int64_t runs_grid = (kRunUserCost * (max_chunks + 1)) / lam + 2;
-  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam));
+  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam,
+                           M::ncf ? kNcfRunChunk : kRunChunk));
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
   // the query-side work that needs no Gram cache, ahead of the join with a pending prepare:
   // NCF k = 16 the per-query MLP prologue (after the layer-1 rows), k <= 16 the d1 table
@@ -3212,11 +3214,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                          c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
     }
   } else {
-    // MF k <= 16: item runs
-    if constexpr (runs)
+    // k <= 16: item runs
+    if constexpr (runs && !M::ncf)
       FIA_HIP_TRY(launch_score_mf_runs(M::K, grid, s, A, Q, c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
                                        c->slices.as<int32_t>(), c->rec.as<double>(), rel_idx, influence, K,
                                        c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), span));
+    if constexpr (runs && M::ncf)
+      FIA_HIP_TRY(launch_score_ncf_runs(M::K, grid, s, A, Q, c->cdesc.as<ChunkDesc>(), c->qbase.as<int64_t>(),
+                                        c->slices.as<int32_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                                        c->cand_pos.as<int32_t>(), c->cand_val.as<double>(), span));
   }
   FIA_HIP_TRY(hipGetLastError());
 topk:

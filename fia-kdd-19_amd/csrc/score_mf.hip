@@ -374,6 +374,173 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))
   }
 }
 
+// ------------------------------------------------------------------------------------
+// k_score_ncf_runs (NCF k <= 16: BASELINE config 3).  The item-run schedule of k_score_mf_runs
+// for NCF (ncf:193-280): descriptor = a chunk of <= kNcfRunChunk = 64 ratings of one side's
+// list + the run of consecutive batch queries sharing that side's entity, one rating per lane
+// (yelp-ex lists hold ~24 ratings: the entity-shared k_score_ncf scored 4 rows per lane and
+// left ~60 % of its lanes idle, after a group build).  Per rating, once per descriptor: the
+// list entries, e_j and the two ReLU masks the Gram pass stored per list position, d1_j =
+// 1[z1 > 0] * T[z2 mask] (k_ncf_d1_table, an L1-resident row) and the other side's gmf row;
+// per query of the run its words by scalar loads (y = W1_side^T x_mlp after k_ncf_rec_y,
+// W3g * x_gmf, the test pair's other id, the header): s_jq = y . d1_j + (W3g x_gmf) . gmf_o,
+// influence, raw buffer stores ranged to the chunk (rel_idx / influence NULL: ranges of 0),
+// the chunk's top-K candidates.
+// ------------------------------------------------------------------------------------
+struct NcfRunArgs {
+  const int32_t* other[2];
+  const float* rating[2];
+  const int32_t* row[2];
+  const int32_t* mask[2];      // per list position: bits [0, k) z1 > 0, [k, 3k/2) z2 > 0
+  const double* resid;         // e_j per list position [side][N]
+  const float* gmf_other[2];   // side 0 (user lists): the item gmf table; side 1: the user gmf table
+  const double* d1tab;         // [2^(k/2)][k]
+  int64_t N;
+};
+
+template <class M, int KM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kRunsWaves))) void k_score_ncf_runs(
+    NcfRunArgs A, int64_t Q, const ChunkDesc* __restrict__ cdesc, const int64_t* __restrict__ qbase,
+    const int32_t* __restrict__ slices, const double* __restrict__ rec, int32_t* __restrict__ rel_idx,
+    double* __restrict__ influence, int K_top, int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
+  static_assert(mask_path<M>() && M::K % 4 == 0, "NCF k in {8, 16}");
+  constexpr int K = M::K, NA = K / 4, CH = kNcfRunChunk;
+  static_assert(CH == 64, "one rating per lane");
+  const int lane = threadIdx.x & 63;
+  const int n_inf = influence ? 8 : 0, n_rel = rel_idx ? 4 : 0;
+  const int64_t nsl = qbase[4 * Q + 1];
+  const int64_t sl = blockIdx.x;
+  if (sl >= nsl) return;
+  int64_t ch = slices[sl];
+  const int64_t cend = slices[sl + 1];
+  if (ch >= cend) return;
+  // list entries of descriptor c (lanes past the chunk's end clamped to its first entry)
+  auto fetch = [&](int64_t c, int32_t& o, float& y, int32_t& rw, double& e, int32_t& mk) {
+    const ChunkDesc dd = cdesc[c];
+    const int sd = dd.side & 0xff;
+    const int64_t p = dd.list_base + (lane < dd.len ? lane : 0);
+    o = A.other[sd][p];
+    y = A.rating[sd][p];
+    rw = A.row[sd][p];
+    e = A.resid[sd * A.N + p];
+    mk = A.mask[sd][p];
+  };
+  int32_t o, row, mk;
+  float y;
+  double e;
+  fetch(ch, o, y, row, e, mk);
+  int64_t nx = ch + 1 < cend ? ch + 1 : -1;
+  while (true) {
+    const ChunkDesc d = cdesc[ch];
+    const int sd = d.side & 0xff, nq = d.side >> 8;
+    const int32_t q0 = d.q;
+    const int len = d.len;
+    // the rating's gathers: the other side's gmf row and its d1 table row
+    float4 g4[NA];
+    double2 t2[K / 2];
+    {
+      const float4* src = reinterpret_cast<const float4*>(A.gmf_other[sd] + (int64_t)o * K);
+#pragma unroll
+      for (int c = 0; c < NA; ++c) g4[c] = src[c];
+      const double2* tr = reinterpret_cast<const double2*>(A.d1tab + (int64_t)(mk >> K) * K);
+#pragma unroll
+      for (int c = 0; c < K / 2; ++c) t2[c] = tr[c];
+    }
+    const bool more = nx >= 0;
+    int32_t no, nrow, nmk;
+    float ny;
+    double ne;
+    fetch(more ? nx : ch, no, ny, nrow, ne, nmk);
+    double g[K], d1[K];
+#pragma unroll
+    for (int c4 = 0; c4 < NA; ++c4) {
+      g[4 * c4 + 0] = (double)g4[c4].x;
+      g[4 * c4 + 1] = (double)g4[c4].y;
+      g[4 * c4 + 2] = (double)g4[c4].z;
+      g[4 * c4 + 3] = (double)g4[c4].w;
+    }
+#pragma unroll
+    for (int c = 0; c < K / 2; ++c) {
+      d1[2 * c] = (mk >> (2 * c)) & 1 ? t2[c].x : 0.0;
+      d1[2 * c + 1] = (mk >> (2 * c + 1)) & 1 ? t2[c].y : 0.0;
+    }
+    asm volatile("" : "+v"(o), "+v"(row));
+    int j = 0;
+    do {
+      const int32_t qj = q0 + j;
+      const double* __restrict__ Rj = rec + (int64_t)qj * M::R;
+      const double* __restrict__ Sj = Rj + 4 + sd * M::SB;
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        s1 = fma(Sj[c], d1[c], s1);
+        s2 = fma(Sj[K + c], g[c], s2);
+      }
+      const double inv_nj = Rj[0], cqj = Rj[1];
+      const int32_t dupj = (int32_t)Sj[2 * K];
+      const int64_t* __restrict__ qb = qbase + 4 * (int64_t)qj;
+      const int64_t ou = qb[0], oi = qb[1], slot0 = qb[2 + sd];
+      const int64_t obj = sd ? oi : ou;
+      double infl = (2.0 * e * (s1 + s2) + cqj) * inv_nj;
+      if (__builtin_expect(__ballot(o == dupj && lane < len) != 0, 0)) {
+        // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (the solve's record)
+        if (o == dupj && lane < len) infl = (2.0 * (Rj[3] - (double)y) * Rj[2] + cqj) * inv_nj;
+      }
+      const int32_t co = (int32_t)(d.out_base - (sd ? qbase[4 * (int64_t)q0 + 1] : qbase[4 * (int64_t)q0]));
+      {
+        const int64_t ob = obj + co;
+        const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<double*>(reinterpret_cast<uintptr_t>(influence) + (uintptr_t)ob * 8), 0, len * n_inf, kBufWord3);
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<int32_t*>(reinterpret_cast<uintptr_t>(rel_idx) + (uintptr_t)ob * 4), 0, len * n_rel, kBufWord3);
+        const long long ib = __double_as_longlong(infl);
+        __builtin_amdgcn_raw_buffer_store_b64(
+            (__attribute__((ext_vector_type(2))) unsigned){(unsigned)(ib & 0xffffffffll), (unsigned)(ib >> 32)}, ri,
+            lane * 8, 0, kBufNT);
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)row, rr, lane * 4, 0, kBufNT);
+      }
+      const int64_t slot = slot0 + co / CH;
+      const int32_t pbj = sd ? (int32_t)(oi - ou) : 0;
+      if constexpr (KM == 1) {
+        double ba = lane < len ? topk_key(infl) : -2.0, bv = infl;
+        int bp = lane;
+        wave_top1_fast(ba, bp, bv);
+        const bool okk = ba > -1.5;
+        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(cand_pos + slot, 0, 4, kBufWord3);
+        const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(cand_val + slot, 0, 8, kBufWord3);
+        const long long vb = __double_as_longlong(okk ? bv : (double)NAN);
+        __builtin_amdgcn_raw_buffer_store_b32((unsigned)(okk ? pbj + co + bp : -1), rp, lane * 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(
+            (__attribute__((ext_vector_type(2))) unsigned){(unsigned)(vb & 0xffffffffll), (unsigned)(vb >> 32)}, rv,
+            lane * 8, 0, 0);
+      } else if constexpr (KM == 2) {
+        const bool ok = lane < len;
+        const int cp = ok ? pbj + co + lane : -1;
+        const double ca = ok ? topk_key(infl) : -2.0;
+        double pa = INFINITY;
+        int pp = -1;
+        for (int t = 0; t < K_top; ++t) {
+          double ba = -2.0, bv = 0.0;
+          int bp = 0x7fffffff;
+          if (cp >= 0 && better(pa, pp, ca, cp) && better(ca, cp, ba, bp)) { ba = ca; bp = cp; bv = infl; }
+          wave_best(ba, bp, bv);
+          if (lane == 0) {
+            const bool okk = ba > -1.5;
+            cand_pos[slot * K_top + t] = okk ? bp : -1;
+            cand_val[slot * K_top + t] = okk ? bv : NAN;
+          }
+          pa = ba;
+          pp = bp;
+        }
+      }
+    } while (++j < nq);
+    if (!more) break;
+    ch = nx;
+    nx = ch + 1 < cend ? ch + 1 : -1;
+    o = no; y = ny; row = nrow; e = ne; mk = nmk;
+  }
+}
+
 }  // namespace
 
 hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& QA, int64_t Q,
@@ -401,6 +568,40 @@ hipError_t launch_score_mf_runs(int k, int64_t grid, hipStream_t s, const QueryA
     return hipErrorInvalidValue;
   }
 #undef FIA_RUNS_LAUNCH
+  return hipGetLastError();
+}
+
+}  // namespace fia
+
+namespace fia {
+
+hipError_t launch_score_ncf_runs(int k, int64_t grid, hipStream_t s, const QueryArgs& QA, int64_t Q,
+                                 const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
+                                 const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
+                                 double* cand_val, PhaseSpan ps) {
+  NcfRunArgs A{};
+  for (int sd = 0; sd < 2; ++sd) {
+    A.other[sd] = QA.other[sd];
+    A.rating[sd] = QA.rating[sd];
+    A.row[sd] = QA.row[sd];
+    A.mask[sd] = reinterpret_cast<const int32_t*>(QA.lgm[sd]);
+    A.gmf_other[sd] = QA.t[sd == 0 ? 3 : 2];
+  }
+  A.resid = QA.lres;
+  A.d1tab = QA.d1tab;
+  A.N = QA.N;
+#define FIA_NRUNS_LAUNCH(KK, KM)                                                                                     \
+  hipExtLaunchKernelGGL((k_score_ncf_runs<NCFm<KK>, KM>), dim3((unsigned)grid), dim3(64), 0, s, ps.a, ps.b, 0, A, Q, \
+                        cdesc, qbase, slices, rec, rel_idx, influence, K, cand_pos, cand_val)
+  const int km = K <= 0 ? 0 : K == 1 ? 1 : 2;
+  if (k == 16) {
+    if (km == 0) FIA_NRUNS_LAUNCH(16, 0); else if (km == 1) FIA_NRUNS_LAUNCH(16, 1); else FIA_NRUNS_LAUNCH(16, 2);
+  } else if (k == 8) {
+    if (km == 0) FIA_NRUNS_LAUNCH(8, 0); else if (km == 1) FIA_NRUNS_LAUNCH(8, 1); else FIA_NRUNS_LAUNCH(8, 2);
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef FIA_NRUNS_LAUNCH
   return hipGetLastError();
 }
 
