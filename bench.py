@@ -624,7 +624,8 @@ def main():
     # launches and the scoring kernel's are timed by HIP events over the timed region
     per_step = {p: v[0] / n_instr for p, v in phases.items()}
     dom = max(("prepare", "solve", "score"), key=lambda p: per_step.get(p, 0.0))
-    ctx.set_profiling(True, phases=tuple(sorted({"score", dom})))
+    if not os.environ.get("FIA_BENCH_NO_EVENTS"):
+        ctx.set_profiling(True, phases=tuple(sorted({"score", dom})))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)

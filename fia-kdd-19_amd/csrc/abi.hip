@@ -152,8 +152,13 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 hipError_t enter_stream(fia_ctx* c, hipStream_t s) {
   if (c->has_stream && c->stream != s) {
     if (hipError_t e = fia::join_prepare(c, c->stream); e != hipSuccess) return e;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(c->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone, ns = hipStreamCaptureStatusNone;
+    // a capture starting on a new stream (a graph captured after eager warm-up on another
+    // stream): no synchronisation is legal inside a global-mode capture, and none is needed
+    // -- nothing can be regrown, so nothing freed, while capturing; the caller has finished
+    // the warm-up stream (fia.h)
+    const bool new_capturing = hipStreamIsCapturing(s, &ns) == hipSuccess && ns != hipStreamCaptureStatusNone;
+    if (!new_capturing && hipStreamIsCapturing(c->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
       hipError_t e = hipStreamSynchronize(c->stream);
       if (e != hipSuccess) return e;
     }

@@ -23,8 +23,8 @@ constexpr int kRsrcWord3 = 0x00020000;
 // the table's buffer range (the hardware returns 0: no masking), the per-sub-batch flags are
 // bits of three wave masks, a segment's count rides in its last descriptor.  A flush stages
 // the packed triangle (+ the bias row: column sums, the count) in LDS and writes it as 16-B
-// stores.  fia_prepare_for marks (MARK): the sub-batches of unmarked entities gather from an
-// empty buffer range, skip their MFMAs and end no segment.
+// stores.  fia_prepare_for marks (MARK): the sub-batches of unmarked entities gather past every
+// table's range, skip their MFMAs and end no segment.
 // Lane map (f64 16x16x4): lane l supplies G[l >> 4][l & 15] of the row-quad as both A (= G^T)
 // and B; C register r = C[(l >> 4) + 4 r][l & 15].
 // ------------------------------------------------------------------------------------
@@ -44,8 +44,10 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
   // unmarked entities), last of a segment, side 1
   const int2 dv = lane < nd ? G.desc[d0 + lane] : int2{1 << 7, 0};
   bool sk = (dv.x >> 7) & 1;
-  if constexpr (MARK) sk = sk || !G.mark[G.moff[(dv.x >> 6) & 1] + (dv.x >> 8)];
+  // (moff picked by a select: a lane-indexed kernel-argument array would go through scratch)
+  if constexpr (MARK) sk = sk || !G.mark[((dv.x >> 6) & 1 ? G.moff[1] : G.moff[0]) + (dv.x >> 8)];
   const uint64_t skipm = __ballot(sk), lastm = __ballot((dv.x >> 5) & 1), sidem = __ballot((dv.x >> 6) & 1);
+  if (MARK && skipm == ~0ull) return;     // no marked entity in the range
   {
     const uint4* __restrict__ src = reinterpret_cast<const uint4*>(G.ids) + (int64_t)d0 * 4;
     uint4 tmp[kGsMaxSub * 4 / 64];
@@ -62,18 +64,22 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.emb_other[0]), 0, G.bytes_other[0], kRsrcWord3);
   const __amdgpu_buffer_rsrc_t rs1 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.emb_other[1]), 0, G.bytes_other[1], kRsrcWord3);
-  const __amdgpu_buffer_rsrc_t rsn = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(G.emb_other[0]), 0, 0, kRsrcWord3);
   // the lane's column bytes; columns >= k land past every table (kGsNoRow-sized offsets + this
   // stay outside the range too)
   const uint32_t cb = col < K ? (uint32_t)col * 4u : 0x80000000u;
   // rows of sub-batch t: quad q, row group grp -> rating 4 q + grp of the sub-batch
   auto rows = [&](int t, float (&v)[4]) {
-    __amdgpu_buffer_rsrc_t rs = (sidem >> t) & 1 ? rs1 : rs0;
-    if constexpr (MARK) rs = (skipm >> t) & 1 ? rsn : rs;
+    const __amdgpu_buffer_rsrc_t rs = (sidem >> t) & 1 ? rs1 : rs0;
+    // MARK: a skipped sub-batch's offsets get the top bit (outside every table).  (A third,
+    // empty resource picked here instead went to scratch and a readfirstlane loop per gather.)
+    const uint32_t sb = MARK && ((skipm >> t) & 1) ? 0x80000000u : 0u;
     const uint4 o4 = sids[(t < nd ? t : 0) * 4 + grp];
     const uint32_t oq[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(oq[q] + cb), 0, 0));
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t off = MARK ? (oq[q] + cb) | sb : oq[q] + cb;
+      v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0));
+    }
   };
   // two accumulators (even / odd row-quads): consecutive MFMAs are independent
   d4_t acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};

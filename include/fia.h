@@ -26,7 +26,10 @@
  *     The context owns only its index, caches and scratch.
  *   - Every call is ordered on `stream` (a hipStream_t passed as void*; NULL =
  *     the null stream).  Use one stream per context.  A context is not
- *     thread-safe; use one context per GPU / process.
+ *     thread-safe; use one context per GPU / process.  A call on a new stream first
+ *     synchronises the previous one -- except when the new stream is being captured
+ *     into a HIP graph (no synchronisation is legal there): finish the previous
+ *     stream's work (e.g. an eager warm-up) before the capture begins.
  *   - Every entry point returns FIA_OK (0) or an error code; no exception
  *     crosses the ABI.  fia_last_error() describes the last failure.
  *   - Ids are int32 in [0, num_users) / [0, num_items); ratings are float32.
