@@ -1457,34 +1457,38 @@ __global__ __launch_bounds__(64) void k_big_finish(int64_t Q, const double* __re
 
 // ------------------------------------------------------------------------------------
 // Entity-shared scoring on the f64 matrix cores (work items from build_groups: one
-// <= kChunk chunk of one entity's list x one block of <= kBigMfmaQB queries with that
+// <= kChunk chunk of one entity's list x one block of <= kBigMfmaQB = 32 queries with that
 // entity).  Per rating:
 //   MF  s_q = x_emb,q . emb_other + x_bias,q
 //   NCF s_q = x_mlp,q . g_mlp,j + (W3g * x_gmf,q) . gmf_other
 //   influence = (2 e_j s_q + c_q) / n_q   (mf:240-246); the test pair's own train row
 //   takes e and s = x.v from the record (bit-identical copies).  A workgroup
 // takes one work item; wave h is scoring pass h (ratings [64 h, 64 h + 64) of the
-// chunk, four 16-rating tiles).  Per tile the scores are one 16 x 16 MFMA product
-// over the dotted length KD (MF: x_emb . emb_other; NCF: x_mlp . g_mlp,j then
-// (W3g * x_gmf) . gmf_other): A = the block's query vectors (LDS, k-major), B = the
-// tile's rating vectors streamed from HBM, four consecutive coordinates per lane
-// (full 128-B lines per row).  Lane (m, g) ends with the scores of rating m against
-// queries g, g + 4, g + 8, g + 12, so each influence store is four 128-B segments.
+// chunk, four 16-rating tiles).  Per tile the scores are 16 x 16 MFMA products over the
+// dotted length KD (MF: x_emb . emb_other; NCF: x_mlp . g_mlp,j then (W3g * x_gmf) .
+// gmf_other): A = a 16-query half of the block's query vectors (LDS, k-major), B = the
+// tile's rating vectors streamed from HBM, four consecutive coordinates per lane (full
+// 128-B lines per row).  A block of more than 16 queries runs both halves on each loaded
+// B operand, so a rating row is read once per 32 queries (the k = 256 rows are 1-3 KB).
+// The LDS holds one K-coordinate segment of the 32 query vectors at a time (NCF: the
+// x_mlp half, then the W3g * x_gmf half): 67.6 KB at k = 256, two workgroups per CU.
+// Lane (m, g) ends with the scores of rating m against queries g, g + 4, g + 8, g + 12 of
+// each half, so each influence store is four 128-B segments.
 // ------------------------------------------------------------------------------------
-constexpr int kBigMfmaQB = 16;
+constexpr int kBigMfmaQB = 32;
 
 template <class M>
 constexpr int score_kd() { return M::ncf ? 2 * M::K : M::K; }
 
 template <class M>
-__global__ __launch_bounds__(256) void k_big_score_mfma(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_big_score_mfma(
     BigArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
     const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
     const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
     int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  constexpr int K = M::K, KD = score_kd<M>(), QB = kBigMfmaQB, XS = QB + 1, NPASS = kScoreRows;
-  static_assert(NPASS == 4, "one wave per scoring pass");
-  __shared__ double Xs[KD * XS];       // Xs[k * XS + j]: coordinate k of query j's vector
+  constexpr int K = M::K, QB = kBigMfmaQB, XS = QB + 1, NPASS = kScoreRows;
+  static_assert(NPASS == 4 && QB == 32, "one wave per scoring pass, two 16-query halves");
+  __shared__ double Xs[K * XS];        // Xs[k * XS + j]: coordinate seg + k of query j's vector
   __shared__ double Qs[QB][6];         // 1/n, c_q, x.v, r-hat, dup_other, x_bias (MF)
   __shared__ int64_t Bs[QB][3];        // influence offset, candidate chunk, position offset
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
@@ -1499,13 +1503,17 @@ __global__ __launch_bounds__(256) void k_big_score_mfma(
     const int64_t gb = gstart[g] + (int64_t)qblk * QB;
     const int64_t gn = gstart[g + 1] - gb;
     const int nq = gn < QB ? (int)gn : QB;
+    // coordinates [seg, seg + K) of the block's side vectors into Xs (zero past nq)
+    auto stage = [&](int seg) {
+      for (int t = tid; t < K * QB; t += 256) {
+        const int j = t / K, k = t - j * K;
+        double v = 0.0;
+        if (j < nq) v = rec[(int64_t)gq[gb + j] * M::R + 8 + sd * M::SB + seg + k];
+        Xs[k * XS + j] = v;
+      }
+    };
     __syncthreads();                   // the previous item's LDS is consumed
-    for (int t = tid; t < KD * QB; t += 256) {
-      const int j = t / KD, k = t - j * KD;
-      double v = 0.0;
-      if (j < nq) v = rec[(int64_t)gq[gb + j] * M::R + 8 + sd * M::SB + k];
-      Xs[k * XS + j] = v;
-    }
+    stage(0);
     if (tid < QB) {
       const int32_t q = gq[gb + (tid < nq ? tid : nq - 1)];
       const double* __restrict__ R = rec + (int64_t)q * M::R;
@@ -1538,127 +1546,153 @@ __global__ __launch_bounds__(256) void k_big_score_mfma(
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) ej[t] = A.resid[rw[t]];
-    d4_t acc[4];
+    d4_t acc[2][4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = d4_t{0.0, 0.0, 0.0, 0.0};
-    // k-groups of 16 coordinates: lane (m, g) holds coordinates 16 G + 4 g + i, i < 4, of
-    // rating m; MFMA step i of the group uses coordinate 16 G + 4 g + i on both sides
-    auto group = [&](int G, const double (&b)[4][4]) {
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double a = Xs[(16 * G + 4 * kl + i) * XS + ml];
+      for (int t = 0; t < 4; ++t) acc[h][t] = d4_t{0.0, 0.0, 0.0, 0.0};
+    // the MFMA passes over one staged segment; TWO: both 16-query halves per B operand
+    // (a uniform branch around whole passes, none inside the MFMA chains)
+    auto segment = [&](auto two, auto seg) {
+      constexpr bool TWO = decltype(two)::value;
+      constexpr bool GM = M::ncf && decltype(seg)::value == 0;   // the g_mlp segment
+      // k-groups of 16 coordinates: lane (m, g) holds coordinates 16 G + 4 g + i, i < 4,
+      // of rating m; MFMA step i of the group uses coordinate 16 G + 4 g + i on both sides
+      auto group = [&](int G, const double (&b)[4][4]) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = mfma4(a, b[t][i], acc[t]);
-      }
-    };
-    if constexpr (M::ncf) {
-      // x_mlp . g_mlp,j: g_mlp rows of this side (fp64)
-      const double* __restrict__ gmr[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) gmr[t] = A.gm[sd] + (int64_t)rw[t] * K + 4 * kl;
-      double bA[4][4], bB[4][4];
-      auto ldg = [&](int G, double (&b)[4][4]) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const double2 u0 = *reinterpret_cast<const double2*>(gmr[t] + 16 * G);
-          const double2 u1 = *reinterpret_cast<const double2*>(gmr[t] + 16 * G + 2);
-          b[t][0] = u0.x; b[t][1] = u0.y; b[t][2] = u1.x; b[t][3] = u1.y;
-        }
-      };
-      ldg(0, bA);
-      for (int G = 0; G < K / 16; G += 2) {
-        ldg(G + 1, bB);
-        group(G, bA);
-        if (G + 2 < K / 16) ldg(G + 2, bA);
-        group(G + 1, bB);
-      }
-    }
-    {
-      // (MF: x_emb, NCF: W3g * x_gmf) . the other side's embedding row (fp32)
-      constexpr int KOFF = M::ncf ? K : 0;
-      const float* __restrict__ T = M::ncf ? (sd == 0 ? A.t[3] : A.t[2]) : (sd == 0 ? A.t[1] : A.t[0]);
-      const float* __restrict__ er[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) er[t] = T + (int64_t)o[t] * K + 4 * kl;
-      float4 fA[4], fB[4];
-      auto lde = [&](int G, float4 (&f)[4]) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t) f[t] = *reinterpret_cast<const float4*>(er[t] + 16 * G);
-      };
-      auto grp = [&](int G, const float4 (&f)[4]) {
-        double b[4][4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          b[t][0] = f[t].x; b[t][1] = f[t].y; b[t][2] = f[t].z; b[t][3] = f[t].w;
-        }
-        group(KOFF / 16 + G, b);
-      };
-      lde(0, fA);
-      for (int G = 0; G < K / 16; G += 2) {
-        lde(G + 1, fB);
-        grp(G, fA);
-        if (G + 2 < K / 16) lde(G + 2, fA);
-        grp(G + 1, fB);
-      }
-    }
-    // influence of rating m against queries kl + 4 r
-    double la[4][4];   // [r][t] top-K keys
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = kl + 4 * r;
-      const double inv_n = Qs[j][0], cq = Qs[j][1], xv = Qs[j][2], rhat = Qs[j][3], dup = Qs[j][4], xb = Qs[j][5];
-      const int64_t obj = Bs[j][0];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        double ss = acc[t][r] + xb, ee = ej[t];
-        if ((double)o[t] == dup) { ee = rhat - (double)y[t]; ss = xv; }
-        const double infl = (2.0 * ee * ss + cq) * inv_n;
-        const int idx = 64 * wave + 16 * t + ml;
-        if (ok[t] && j < nq) {
-          if (influence) influence[obj + idx] = infl;
-          if (rel_idx) rel_idx[obj + idx] = rw[t];
-        }
-        acc[t][r] = infl;
-        la[r][t] = ok[t] ? topk_key(infl) : -2.0;
-      }
-    }
-    if (K_top > 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = kl + 4 * r;
-        const int64_t cbj = Bs[j][1], poj = Bs[j][2];
-        double pa = INFINITY;
-        int pp = -1;
-        for (int tt = 0; tt < K_top; ++tt) {
-          double ba = -2.0, bv = 0.0;
-          int bp = 0x7fffffff;
+        for (int i = 0; i < 4; ++i) {
+          const double* __restrict__ xr = Xs + (16 * G + 4 * kl + i) * XS + ml;
+          const double a0 = xr[0];
+          const double a1 = TWO ? xr[16] : 0.0;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            const int lp = ok[t] ? cidx * kChunk + 64 * wave + 16 * t + ml : -1;
-            if (lp >= 0 && better(pa, pp, la[r][t], lp) && better(la[r][t], lp, ba, bp)) {
-              ba = la[r][t];
-              bp = lp;
-              bv = acc[t][r];
-            }
+            acc[0][t] = mfma4(a0, b[t][i], acc[0][t]);
+            if constexpr (TWO) acc[1][t] = mfma4(a1, b[t][i], acc[1][t]);
           }
+        }
+      };
+      if constexpr (GM) {
+        // x_mlp . g_mlp,j: g_mlp rows of this side (fp64)
+        const double* __restrict__ gmr[4];
 #pragma unroll
-          for (int off = 8; off > 0; off >>= 1) {   // within the 16 lanes of query j
-            const double oa = __shfl_xor(ba, off);
-            const int op = __shfl_xor(bp, off);
-            const double ov = __shfl_xor(bv, off);
-            if (better(oa, op, ba, bp)) { ba = oa; bp = op; bv = ov; }
+        for (int t = 0; t < 4; ++t) gmr[t] = A.gm[sd] + (int64_t)rw[t] * K + 4 * kl;
+        double bA[4][4], bB[4][4];
+        auto ldg = [&](int G, double (&b)[4][4]) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const double2 u0 = *reinterpret_cast<const double2*>(gmr[t] + 16 * G);
+            const double2 u1 = *reinterpret_cast<const double2*>(gmr[t] + 16 * G + 2);
+            b[t][0] = u0.x; b[t][1] = u0.y; b[t][2] = u1.x; b[t][3] = u1.y;
           }
-          if (ml == 0 && j < nq) {
-            const bool okk = ba > -1.5;
-            const int64_t slot = (cbj * NPASS + wave) * K_top + tt;
-            cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
-            cand_val[slot] = okk ? bv : NAN;
+        };
+        ldg(0, bA);
+        for (int G = 0; G < K / 16; G += 2) {
+          ldg(G + 1, bB);
+          group(G, bA);
+          if (G + 2 < K / 16) ldg(G + 2, bA);
+          group(G + 1, bB);
+        }
+      } else {
+        // (MF: x_emb, NCF: W3g * x_gmf) . the other side's embedding row (fp32)
+        const float* __restrict__ T = M::ncf ? (sd == 0 ? A.t[3] : A.t[2]) : (sd == 0 ? A.t[1] : A.t[0]);
+        const float* __restrict__ er[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) er[t] = T + (int64_t)o[t] * K + 4 * kl;
+        float4 fA[4], fB[4];
+        auto lde = [&](int G, float4 (&f)[4]) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) f[t] = *reinterpret_cast<const float4*>(er[t] + 16 * G);
+        };
+        auto grp = [&](int G, const float4 (&f)[4]) {
+          double b[4][4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            b[t][0] = f[t].x; b[t][1] = f[t].y; b[t][2] = f[t].z; b[t][3] = f[t].w;
           }
-          pa = ba;
-          pp = bp;
+          group(G, b);
+        };
+        lde(0, fA);
+        for (int G = 0; G < K / 16; G += 2) {
+          lde(G + 1, fB);
+          grp(G, fA);
+          if (G + 2 < K / 16) lde(G + 2, fA);
+          grp(G + 1, fB);
         }
       }
+    };
+    const bool two = nq > 16;
+    auto passes = [&](auto seg) {
+      if (two) segment(std::integral_constant<bool, true>{}, seg);
+      else segment(std::integral_constant<bool, false>{}, seg);
+    };
+    passes(std::integral_constant<int, 0>{});
+    if constexpr (M::ncf) {
+      __syncthreads();                 // every wave is done with the x_mlp segment
+      stage(K);
+      __syncthreads();
+      passes(std::integral_constant<int, 1>{});
     }
+    // influence of rating m against queries h0 + kl + 4 r of one half
+    auto epilogue = [&](d4_t (&ac)[4], int h0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = h0 + kl + 4 * r;
+        const double inv_n = Qs[j][0], cq = Qs[j][1], xv = Qs[j][2], rhat = Qs[j][3], dup = Qs[j][4], xb = Qs[j][5];
+        const int64_t obj = Bs[j][0];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          double ss = ac[t][r] + xb, ee = ej[t];
+          if ((double)o[t] == dup) { ee = rhat - (double)y[t]; ss = xv; }
+          const double infl = (2.0 * ee * ss + cq) * inv_n;
+          const int idx = 64 * wave + 16 * t + ml;
+          if (ok[t] && j < nq) {
+            if (influence) influence[obj + idx] = infl;
+            if (rel_idx) rel_idx[obj + idx] = rw[t];
+          }
+          ac[t][r] = infl;
+        }
+      }
+      if (K_top > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = h0 + kl + 4 * r;
+          const int64_t cbj = Bs[j][1], poj = Bs[j][2];
+          double pa = INFINITY;
+          int pp = -1;
+          for (int tt = 0; tt < K_top; ++tt) {
+            double ba = -2.0, bv = 0.0;
+            int bp = 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int lp = ok[t] ? cidx * kChunk + 64 * wave + 16 * t + ml : -1;
+              const double key = topk_key(ac[t][r]);     // (recomputed: no key registers)
+              if (lp >= 0 && better(pa, pp, key, lp) && better(key, lp, ba, bp)) {
+                ba = key;
+                bp = lp;
+                bv = ac[t][r];
+              }
+            }
+#pragma unroll
+            for (int off = 8; off > 0; off >>= 1) {   // within the 16 lanes of query j
+              const double oa = __shfl_xor(ba, off);
+              const int op = __shfl_xor(bp, off);
+              const double ov = __shfl_xor(bv, off);
+              if (better(oa, op, ba, bp)) { ba = oa; bp = op; bv = ov; }
+            }
+            if (ml == 0 && j < nq) {
+              const bool okk = ba > -1.5;
+              const int64_t slot = (cbj * NPASS + wave) * K_top + tt;
+              cand_pos[slot] = okk ? (int32_t)(bp + poj) : -1;
+              cand_val[slot] = okk ? bv : NAN;
+            }
+            pa = ba;
+            pp = bp;
+          }
+        }
+      }
+    };
+    epilogue(acc[0], 0);
+    if (two) epilogue(acc[1], 16);
   }
 }
 
