@@ -91,8 +91,9 @@ def parse(argv=None):
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
     ap.add_argument("--spinup-seconds", type=float, default=None,
                     help="untimed steps for at least this long before the warmup (default: 20 for the 20M configs, "
-                         "0 otherwise): a fresh MI355X runs the HBM-heavy scoring kernels ~15 %% slower for its "
-                         "first ~30 s of load")
+                         "1 otherwise): a fresh MI355X runs the HBM-heavy scoring kernels ~15 %% slower for its "
+                         "first ~30 s of load, and the sub-ms ml-1m-ex / yelp-ex steps ~4 %% slower over the "
+                         "driver's 5 + 20 steps than after 1 s of load (same-box A/B, tools/evt_ab.sh)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rank-set", type=int, default=0,
@@ -580,7 +581,7 @@ def main():
                 a, b = a.cpu(), b.cpu()
             tg.start(a, b)
 
-    spinup = args.spinup_seconds if args.spinup_seconds is not None else (20.0 if cfg["data"] == "20m" else 0.0)
+    spinup = args.spinup_seconds if args.spinup_seconds is not None else (20.0 if cfg["data"] == "20m" else 1.0)
     t_spin = time.time()
     n_spin = 0
     while time.time() - t_spin < spinup:
