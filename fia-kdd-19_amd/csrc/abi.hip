@@ -429,9 +429,11 @@ static int query_batch_common(fia_ctx* c, int64_t Q, const int32_t* qu, const in
     // (small k joins the pending Gram pass right before its solve, after the query scans)
     if (fia::big_supported(c->p.model, c->p.k))
       if (hipError_t es = fia::join_prepare(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
-    // chunk descriptors / candidate slots: at most 2 per query + one per kNcfRunChunk ratings
-    // (the shortest run chunk)
-    const int64_t max_chunks = 2 * Q + total_rel / fia::kNcfRunChunk + 1;
+    // chunk descriptors / candidate slots: at most 2 per query + one per chunk of the model's
+    // shortest chunk length (NCF k <= 16 runs: kNcfRunChunk; else kRunChunk).  (A tighter bound
+    // also keeps ml-1m-ex's top-K merge on its thread-per-query kernel.)
+    const int64_t clen = c->p.model == FIA_MODEL_NCF && c->p.k <= 16 ? fia::kNcfRunChunk : fia::kRunChunk;
+    const int64_t max_chunks = 2 * Q + total_rel / clen + 1;
     bool unsup = false;
     hipError_t e = fia::query_model(c, Q, qu, qi, offsets, max_chunks, rel_idx, influence, x_out, K, topk_pos,
                                     topk_idx, topk_val, as_stream(stream), unsup, x_in);
