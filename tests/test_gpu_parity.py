@@ -477,24 +477,85 @@ def test_cached_inverse_hvp_force_refresh_false_large_k(model, k, tmp_path):
             assert fh.read() == ref_bytes
 
 
+@pytest.mark.parametrize("model", ["MF", "NCF"])
 @pytest.mark.parametrize("k", [8, 16])
 @pytest.mark.parametrize("K", [1, 4])
-def test_mf_small_k_topk_only_no_outputs(k, K, tmp_path):
+def test_small_k_topk_only_no_outputs(model, k, K, tmp_path):
     """fia_query_batch with rel_idx = influence = NULL (get_influence_batch(full=False)): the
-    MF k <= 16 item-run kernel drops every per-rating store (zero-length buffer ranges) and the
-    top-K lists equal the full run's."""
+    k <= 16 item-run kernels (k_score_mf_runs, k_score_ncf_runs) drop every per-rating store
+    (zero-length buffer ranges) and the top-K lists equal the full run's."""
     rng = np.random.default_rng(40 + k)
     U, I, N = 500, 60, 6000
     key = np.sort(rng.choice(U * I, N, replace=False))
     tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
     tr = rng.integers(1, 6, N).astype(np.float32)
-    p = synth.mf_params(U, I, k, 4)
+    p = (synth.mf_params if model == "MF" else synth.ncf_params)(U, I, k, 4)
     qi = np.sort(rng.integers(0, I, 200)).astype(np.int32)      # item runs
     qu = rng.integers(0, U, 200).astype(np.int32)
-    m = make_model("MF", U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    m = make_model(model, U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
     full = m.get_influence_batch(list(range(qu.size)), K=K)
     lean = m.get_influence_batch(list(range(qu.size)), K=K, full=False, return_x=False)
     assert "influence" not in lean and "rel_idx" not in lean
     for key_ in ("topk_pos", "topk_idx"):
         assert np.array_equal(lean[key_], full[key_]), key_
     assert np.array_equal(lean["topk_val"], full["topk_val"], equal_nan=True)
+
+
+@pytest.mark.parametrize("model", ["MF", "NCF"])
+def test_graph_capture_matches_eager(model):
+    """fia_prepare + fia_count_related + fia_query_batch captured into one HIP graph after an
+    eager warm-up on another stream (as `bench.py --graph` does: the capture starts on a new
+    stream, which the ABI must not synchronise against) and replayed: every output equals the
+    eager run's bit for bit."""
+    import torch
+    from influence import _lib
+    rng = np.random.default_rng(77)
+    U, I, N, k = 400, 80, 8000, 16
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = (synth.mf_params if model == "MF" else synth.ncf_params)(U, I, k, 7)
+    qi_np = np.sort(rng.integers(0, I, 300)).astype(np.int32)
+    qu_np = rng.integers(0, U, 300).astype(np.int32)
+    dev = torch.device("cuda:0")
+    ctx = _lib.Context(0)
+    tables = [torch.from_numpy(np.ascontiguousarray(p[n], np.float32)).to(dev) for n in p]
+    ctx.set_params(_lib.FIA_MODEL_MF if model == "MF" else _lib.FIA_MODEL_NCF, k, U, I, tables, 1e-3, 1e-6)
+    ctx.build_index(torch.from_numpy(tu).to(dev), torch.from_numpy(ti).to(dev), torch.from_numpy(tr).to(dev), U, I)
+    qu, qi = torch.from_numpy(qu_np).to(dev), torch.from_numpy(qi_np).to(dev)
+    off, tot = ctx.count_related(qu, qi)
+    D, K, Q = ctx.num_params(), 3, qu_np.size
+
+    def bufs():
+        return dict(rel=torch.full((tot,), -7, dtype=torch.int32, device=dev),
+                    infl=torch.full((tot,), float("nan"), dtype=torch.float64, device=dev),
+                    x=torch.zeros(Q * D, dtype=torch.float64, device=dev),
+                    tp=torch.zeros(Q * K, dtype=torch.int64, device=dev),
+                    tix=torch.zeros(Q * K, dtype=torch.int64, device=dev),
+                    tv=torch.zeros(Q * K, dtype=torch.float64, device=dev))
+
+    def step(b):
+        ctx.prepare()
+        ctx.count_related(qu, qi, off, want_total=False)
+        ctx.query_batch(qu, qi, off, tot, b["rel"], b["infl"], b["x"], K, b["tp"], b["tix"], b["tv"])
+
+    eager = bufs()
+    step(eager)
+    torch.cuda.synchronize(dev)
+    rep = bufs()
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        step(rep)
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    for v in rep.values():
+        v.zero_()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step(rep)
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    for name in eager:
+        a, b = eager[name].cpu().numpy(), rep[name].cpu().numpy()
+        assert np.array_equal(a, b, equal_nan=True), name
