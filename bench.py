@@ -89,6 +89,10 @@ def parse(argv=None):
                     help="with --shard-of S at N=1: which shard (0 .. S-1) to answer")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
+    ap.add_argument("--no-timed-events", action="store_true",
+                    help="A/B only: no HIP-event pair around the scoring kernel in the timed steps (the "
+                         "roofline then falls back to the instrumented steps' kernel time); the pair costs "
+                         "~4 us per ml-1m-ex step")
     ap.add_argument("--spinup-seconds", type=float, default=None,
                     help="untimed steps for at least this long before the warmup (default: 20 for the 20M configs, "
                          "1 otherwise): a fresh MI355X runs the HBM-heavy scoring kernels ~15 %% slower for its "
@@ -625,7 +629,7 @@ def main():
     # launches and the scoring kernel's are timed by HIP events over the timed region
     per_step = {p: v[0] / n_instr for p, v in phases.items()}
     dom = max(("prepare", "solve", "score"), key=lambda p: per_step.get(p, 0.0))
-    if not os.environ.get("FIA_BENCH_NO_EVENTS"):
+    if not args.no_timed_events:
         ctx.set_profiling(True, phases=tuple(sorted({"score", dom})))
     if world > 1:
         dist.barrier()

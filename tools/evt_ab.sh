@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/evt
 for i in 1 2; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --steps 200 --warmup 20 > gpurun_out/evt/ev_$i.json 2>&1 || exit 1
-  FIA_BENCH_NO_EVENTS=1 timeout -k 10 200 python bench.py --no-cpu-baseline --steps 200 --warmup 20 > gpurun_out/evt/noev_$i.json 2>&1 || exit 1
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-timed-events --steps 200 --warmup 20 > gpurun_out/evt/noev_$i.json 2>&1 || exit 1
   timeout -k 10 200 python bench.py --no-cpu-baseline --steps 200 --warmup 20 --graph > gpurun_out/evt/graph_$i.json 2>&1 || exit 1
   timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/evt/d20_$i.json 2>&1 || exit 1
   timeout -k 10 200 python bench.py --no-cpu-baseline --spinup-seconds 1 > gpurun_out/evt/d20spin_$i.json 2>&1 || exit 1
