@@ -2949,8 +2949,10 @@ constexpr bool solve_covered() {
 }
 
 // MF k <= 16 item runs: slice cost target (descriptor cost units per one-wave slice; ml-1m-ex
-// same-box A/B, scoring us: 8 -> 69.4, 16 -> 68.6, 32 -> 73.5, 64 -> 78.6)
-constexpr int kRunLambda = 16;
+// same-box A/B, scoring us -- round 4: 8 -> 69.4, 16 -> 68.6, 32 -> 73.5, 64 -> 78.6; round 5
+// (this kernel): 4 -> 62.0, 8 -> 58.0-58.6, 16 -> 58.8; chunks of 64 / 192 / 256 ratings at
+// 8: 66.3 / 62.0 / 85.8 vs 128; runs of <= 32 queries: 62.6)
+constexpr int kRunLambda = 8;
 
 // MF k <= 16: the Gram stream (its descriptors carry the entity in 24 bits)
 template <class M>
