@@ -36,8 +36,11 @@ constexpr int kPrepThreads = 256;        // Gram workgroup
 constexpr int kSolveThreads = 64;        // one wave per query solve
 constexpr int kGramChunk = 256;          // list rows per Gram work item (MI355X sweep: 64/128/256/512)
 constexpr int kGsSub = 16;              // ratings per Gram-stream sub-batch (4 f64 MFMA row-quads)
-constexpr int kGsSlice = 256;           // longest Gram-stream segment (longer lists: partial slices)
-constexpr int kGsTarget = 16;           // sub-batches per Gram-stream wave (a range closes at >= this)
+constexpr int kGsSlice = 256;           // longest Gram-stream segment (longer lists: partial slices;
+                                        // <= 511: a segment's count rides in 9 bits of its descriptor)
+constexpr int kGsTarget = 8;            // sub-batches per Gram-stream wave (a range closes at >= this)
+// (ml-1m-ex same-box A/B, ms per step: target 16 0.1460-0.1461; 8 0.1446-0.1448; 32 0.1442-0.1453;
+//  slices of 128 0.1483; at most 8 segments per range 0.1481)
 constexpr uint32_t kGsNoRow = 0x7fffff00u;   // Gram-stream row offset of no rating: outside any
                                              // table's buffer range, even + a lane's column bytes
 constexpr int kGsRing = 8;              // gathered sub-batches in the kernel's register ring
@@ -47,6 +50,7 @@ constexpr int kGsMaxSeg = 4;            // most segments (Grams) of one wave's r
 constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
 constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
+static_assert(kGsSlice < 512, "a Gram-stream segment's count rides in 9 bits of its descriptor (out >> 23)");
 
 // Device buffer with grow-on-demand capacity (never shrinks), allocated from the
 // device's stream-ordered pool on the context's stream: growing a buffer frees the old
