@@ -148,12 +148,15 @@ def load_data(cfg):
 
 
 def solve_kernel(cfg):
-    """The library's side-system solve for this config (models.hip query_impl / bigk.hip)."""
+    """The library's side-system solve for this config (models.hip query_impl's use_quad_solve /
+    use_tps / pair_layout / use_col_solve / use_tile_solve, bigk.hip query_big_impl)."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_bs_trail"              # batched blocked LDL^T panels (+ k_bs_dupd/dfac/back)
-    if model == "MF" and k <= 16:
-        return "k_solve_tps"
+    if model == "MF" and k == 16:
+        return "k_solve_quad"            # a quad of lanes per side system
+    if model == "MF" and k <= 8:
+        return "k_solve_tps"             # a thread per side system
     if model == "NCF" and k == 16:
         return "k_solve_rows"            # (+ k_ncf_query_pro, the thread-per-query MLP prologue)
     if model == "NCF" and k == 8:
@@ -162,10 +165,15 @@ def solve_kernel(cfg):
 
 
 def prepare_kernel(cfg):
+    """The library's Gram pass for this config (models.hip prepare_impl, bigk.hip prepare_big).
+    MF k <= 16 is two kernels: the Gram stream and the combine of sliced lists' partial Grams
+    (traffic.json holds their sum per step as the "prepare_phase" entry)."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_big_gram"
-    return "k_ncf_gram_rows" if model == "NCF" else "k_gram_mf_mfma"
+    if model == "NCF":
+        return "k_ncf_gram_rows"
+    return "k_gram_mf_stream + k_gram_combine" if k <= 16 else "k_gram_mf_mfma"
 
 
 def side_dim(model, k):
@@ -180,12 +188,14 @@ def solve_flops(model, k, Q):
     return 2.0 * Q * (2.0 * Dd ** 3 / 3.0 + 2.0 * Dd * Dd)
 
 
-def prepare_flops(model, k, N):
-    """Entity Gram caches: per rating and side a symmetric rank-1 update, D_s(D_s+1)/2
-    multiply-adds (+ for NCF the ~12 k^2 flops of the per-rating MLP)."""
+def prepare_flops(model, k, rows):
+    """Entity Gram caches: per list entry (a rating in its user's or its item's list) a
+    symmetric rank-1 update, D_s(D_s+1)/2 multiply-adds (+ for NCF the ~12 k^2 flops of the
+    per-rating MLP).  rows = the list entries of the cached entities: 2N for the
+    full prepare, the marked users' and items' list lengths for a shard's fia_prepare_for."""
     Dd = float(side_dim(model, k))
     per = Dd * (Dd + 1.0) + (12.0 * k * k if model == "NCF" else 0.0)
-    return 2.0 * N * per
+    return float(rows) * per
 
 
 def score_kernel(cfg, K=1):
@@ -671,7 +681,10 @@ def main():
     score_ms = timed_ms("score")
     kern = score_kernel(cfg, K)
     alg_bytes = float(bytes_per_query(cfg["model"], k, n_q).sum()) / len(batches)   # mean per launch
-    tj = load_traffic(args.traffic_json, args.config, kern)
+    # a shard's kernels move the shard's bytes: its own traffic.json key (none: traffic null)
+    tkey = args.config if shard_of == 1 else "%s/shard%dof%d" % (
+        args.config, rank if world > 1 else args.shard_index, shard_of)
+    tj = load_traffic(args.traffic_json, tkey, kern)
     traffic = tj.get("hbm_bytes_per_launch") if tj else None
     deg_u = np.bincount(tu, minlength=U).astype(np.float64)
     deg_i = np.bincount(ti, minlength=I).astype(np.float64)
@@ -696,13 +709,18 @@ def main():
             fmodel = "2 side systems per query of D_s = %d: LDL^T 2D^3/3 + solves 2D^2 flops" % side_dim(cfg["model"], k)
         else:
             dk = prepare_kernel(cfg)
-            flops = prepare_flops(cfg["model"], k, int(tu.size))
-            fmodel = "per rating and side: Gram rank-1 update D_s(D_s+1) flops (+ NCF MLP 12 k^2)"
+            # the list entries of the cached entities (a shard caches only its queries' users
+            # and items)
+            rows = float(deg_u[np.unique(qu_np)].sum() + deg_i[np.unique(qi_np)].sum()) if sharded \
+                else 2.0 * tu.size
+            flops = prepare_flops(cfg["model"], k, rows)
+            fmodel = ("per list entry of the %s entities (%d entries): Gram rank-1 update D_s(D_s+1) flops "
+                      "(+ NCF MLP 12 k^2)" % ("shard's cached" if sharded else "cached", rows))
         # PMC bytes of the whole phase per launch when recorded (the solve phase is several
         # kernels, dispatched many times per batch: "<phase>_phase" entries sum them), else the
         # dominant kernel's own entry
-        dtj = load_traffic(args.traffic_json, args.config, dom + "_phase") or \
-            load_traffic(args.traffic_json, args.config, dk)
+        dtj = load_traffic(args.traffic_json, tkey, dom + "_phase") or \
+            load_traffic(args.traffic_json, tkey, dk)
         dtraffic = dtj.get("hbm_bytes_per_launch") if dtj else None
         tfs = flops / (ph_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",

@@ -149,23 +149,33 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // invalidate a capture on) other contexts' streams.  A previous stream that is capturing
 // cannot be synchronised; nothing of ours can be freed under it (DevBuf::reserve refuses to
 // regrow during a capture).
-hipError_t enter_stream(fia_ctx* c, hipStream_t s) {
+// A capture cannot start while a Gram pass forked onto the context's aux stream by an eager
+// fia_prepare / fia_prepare_for is still unjoined: the captured kernels would have no edge to
+// it (an event recorded outside the capture is no graph dependency, and no host wait is legal
+// inside a global-mode capture), so a replay could read Gram caches still being written.
+// That call fails with FIA_ERR_STATE; a joining call (fia_query_batch or fia_prepare) on a
+// non-capturing stream clears the condition.
+int enter_stream(fia_ctx* c, hipStream_t s, const char* where) {
+  hipStreamCaptureStatus ns = hipStreamCaptureStatusNone;
+  const bool new_capturing = hipStreamIsCapturing(s, &ns) == hipSuccess && ns != hipStreamCaptureStatusNone;
+  if (new_capturing && c->prep_pending)
+    return fail(c, FIA_ERR_STATE,
+                std::string(where) + ": a forked Gram pass of an earlier eager fia_prepare is not joined yet; "
+                "call fia_query_batch (or fia_prepare) on a non-capturing stream before starting a capture");
   if (c->has_stream && c->stream != s) {
-    if (hipError_t e = fia::join_prepare(c, c->stream); e != hipSuccess) return e;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone, ns = hipStreamCaptureStatusNone;
+    if (hipError_t e = fia::join_prepare(c, c->stream); e != hipSuccess) return hip_fail(c, e, where);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     // a capture starting on a new stream (a graph captured after eager warm-up on another
     // stream): no synchronisation is legal inside a global-mode capture, and none is needed
     // -- nothing can be regrown, so nothing freed, while capturing; the caller has finished
     // the warm-up stream (fia.h)
-    const bool new_capturing = hipStreamIsCapturing(s, &ns) == hipSuccess && ns != hipStreamCaptureStatusNone;
     if (!new_capturing && hipStreamIsCapturing(c->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
-      hipError_t e = hipStreamSynchronize(c->stream);
-      if (e != hipSuccess) return e;
+      if (hipError_t e = hipStreamSynchronize(c->stream); e != hipSuccess) return hip_fail(c, e, where);
     }
   }
   c->stream = s;
   c->has_stream = true;
-  return hipSuccess;
+  return FIA_OK;
 }
 
 }  // namespace
@@ -197,12 +207,14 @@ int fia_destroy(fia_ctx* c) {
     // so the frees complete before the context goes.  A context that never saw a stream owns
     // no device buffer.  (Destroying a context while its stream is being captured leaves its
     // buffers to the pool: they cannot be freed inside someone else's capture.)
-    if (c->aux) (void)hipStreamSynchronize(c->aux);
-    c->prep_pending = c->l1_pending = false;
     const hipStream_t ds = c->has_stream ? c->stream : nullptr;
     hipStreamCaptureStatus dcs = hipStreamCaptureStatusNone;
-    const bool can_free = c->has_stream && hipStreamIsCapturing(ds, &dcs) == hipSuccess &&
-                          dcs == hipStreamCaptureStatusNone;
+    const bool capturing = c->has_stream && !(hipStreamIsCapturing(ds, &dcs) == hipSuccess &&
+                                              dcs == hipStreamCaptureStatusNone);
+    const bool can_free = c->has_stream && !capturing;
+    // (inside a capture no host wait is legal: the aux stream, like the buffers, is left)
+    if (c->aux && !capturing) (void)hipStreamSynchronize(c->aux);
+    c->prep_pending = c->l1_pending = false;
     if (can_free) (void)hipStreamSynchronize(ds);
     auto rel = [&](fia::DevBuf& b) {
       if (can_free) b.release(ds);
@@ -221,7 +233,7 @@ int fia_destroy(fia_ctx* c) {
                            &c->cpllist, &c->lscr, &c->mark, &c->d1tab, &c->slices, &c->wfrag};
     for (auto* b : bufs) rel(*b);
     if (can_free) (void)hipStreamSynchronize(ds);   // the stream-ordered frees complete
-    if (c->aux) (void)hipStreamDestroy(c->aux);
+    if (c->aux && !capturing) (void)hipStreamDestroy(c->aux);
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->l1_ev) (void)hipEventDestroy(c->l1_ev);
     if (c->prep_ev) (void)hipEventDestroy(c->prep_ev);
@@ -285,7 +297,7 @@ int fia_build_index(fia_ctx* c, int64_t N, int64_t U, int64_t I, const int32_t* 
     if (c->p.valid && (c->p.U != U || c->p.I != I))
       return fail(c, FIA_ERR_INVALID, "num_users/num_items differ from the registered params");
     DeviceGuard g(c->device);
-    if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_build_index");
+    if (int rc = enter_stream(c, as_stream(stream), "fia_build_index"); rc != FIA_OK) return rc;
     if (hipError_t es = fia::join_prepare(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_build_index");
     std::string why;
     hipError_t e = fia::build_index(c, N, U, I, user, item, rating, as_stream(stream), why);
@@ -305,7 +317,7 @@ int fia_prepare(fia_ctx* c, void* stream) {
     if (!c->idx.valid) return fail(c, FIA_ERR_STATE, "fia_build_index has not been called");
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
-    if (hipError_t es = enter_stream(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare");
+    if (int rc = enter_stream(c, s, "fia_prepare"); rc != FIA_OK) return rc;
     if (hipError_t es = fia::join_prepare(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare");
     bool unsup = false;
     // small k: the Gram pass on the aux stream (the large-k prepare synchronises inside)
@@ -332,7 +344,7 @@ int fia_prepare_for(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi,
     if (Q > 0 && (!qu || !qi)) return fail(c, FIA_ERR_INVALID, "null query array");
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
-    if (hipError_t es = enter_stream(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare_for");
+    if (int rc = enter_stream(c, s, "fia_prepare_for"); rc != FIA_OK) return rc;
     // the marks below are read by a still-queued Gram pass
     if (hipError_t es = fia::join_prepare(c, s); es != hipSuccess) return hip_fail(c, es, "fia_prepare_for");
     bool unsup = false;
@@ -368,8 +380,8 @@ int fia_count_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     if (!offsets || (Q > 0 && (!qu || !qi))) return fail(c, FIA_ERR_INVALID, "null query array");
     DeviceGuard g(c->device);
     hipStream_t s = as_stream(stream);
-    hipError_t e = enter_stream(c, s);
-    if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
+    if (int rc = enter_stream(c, s, "fia_count_related"); rc != FIA_OK) return rc;
+    hipError_t e = hipSuccess;
     if (total_out) {
       e = c->flag.reserve(64, s);
       if (e != hipSuccess) return hip_fail(c, e, "fia_count_related");
@@ -403,7 +415,7 @@ int fia_related(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, con
     if (Q < 0 || Q >= (1LL << 31)) return fail(c, FIA_ERR_INVALID, "num_queries out of range");
     if (Q > 0 && (!qu || !qi || !offsets || !rel_idx)) return fail(c, FIA_ERR_INVALID, "null array");
     DeviceGuard g(c->device);
-    if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_related");
+    if (int rc = enter_stream(c, as_stream(stream), "fia_related"); rc != FIA_OK) return rc;
     hipError_t e = fia::write_related(c, Q, qu, qi, offsets, rel_idx, as_stream(stream));
     if (e != hipSuccess) return hip_fail(c, e, "fia_related");
     return FIA_OK;
@@ -425,7 +437,7 @@ static int query_batch_common(fia_ctx* c, int64_t Q, const int32_t* qu, const in
     if (K > 0 && (!topk_pos || !topk_idx || !topk_val)) return fail(c, FIA_ERR_INVALID, "null top-K output");
     if (Q == 0) return FIA_OK;
     DeviceGuard g(c->device);
-    if (hipError_t es = enter_stream(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");
+    if (int rc = enter_stream(c, as_stream(stream), "fia_query_batch"); rc != FIA_OK) return rc;
     // (small k joins the pending Gram pass right before its solve, after the query scans)
     if (fia::big_supported(c->p.model, c->p.k))
       if (hipError_t es = fia::join_prepare(c, as_stream(stream)); es != hipSuccess) return hip_fail(c, es, "fia_query_batch");

@@ -49,6 +49,7 @@ constexpr int kGsMaxSeg = 4;            // most segments (Grams) of one wave's r
                                         // stored when the range is done
 constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
 constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
+constexpr int kWgBlocks = 4;            // query blocks (one per wave) sharing a workgroup's gathered rows
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)
 static_assert(kGsSlice < 512, "a Gram-stream segment's count rides in 9 bits of its descriptor (out >> 23)");
 
@@ -357,6 +358,12 @@ hipError_t launch_score_ncf_runs(int k, int64_t grid, hipStream_t s, const Query
                                  const ChunkDesc* cdesc, const int64_t* qbase, const int32_t* slices,
                                  const double* rec, int32_t* rel_idx, double* influence, int K, int32_t* cand_pos,
                                  double* cand_val, PhaseSpan ps);
+// MF k in {32, 64}, top-K <= 1 entity-shared f64-MFMA scoring (score_mfma.hip); full = both
+// per-rating outputs present
+hipError_t launch_score_mf_mfma(int k, bool full, int64_t grid, hipStream_t s, PhaseSpan ps, const QueryArgs& A,
+                                int64_t nE, const int64_t* wstart, const int32_t* witems, const int64_t* gstart,
+                                const int32_t* gq, const int64_t* qbase, const double* rec, int32_t* rel_idx,
+                                double* influence, int K, int32_t* cand_pos, double* cand_val);
 // per-query merge of chunk top-K candidates (models.hip); spc = candidate slot sets per chunk
 hipError_t launch_topk_merge(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, int K, int spc,
                              int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,

@@ -70,14 +70,16 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
   // rows of sub-batch t: quad q, row group grp -> rating 4 q + grp of the sub-batch
   auto rows = [&](int t, float (&v)[4]) {
     const __amdgpu_buffer_rsrc_t rs = (sidem >> t) & 1 ? rs1 : rs0;
-    // MARK: a skipped sub-batch's offsets get the top bit (outside every table).  (A third,
-    // empty resource picked here instead went to scratch and a readfirstlane loop per gather.)
-    const uint32_t sb = MARK && ((skipm >> t) & 1) ? 0x80000000u : 0u;
+    // a look-ahead gather past the range's end (t >= nd) and, MARK, a skipped sub-batch get the
+    // top offset bit: outside every table, the hardware returns 0 without touching memory.  (A
+    // third, empty resource picked here instead went to scratch and a readfirstlane loop per
+    // gather.)
+    const uint32_t sb = t >= nd || (MARK && ((skipm >> t) & 1)) ? 0x80000000u : 0u;
     const uint4 o4 = sids[(t < nd ? t : 0) * 4 + grp];
     const uint32_t oq[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t off = MARK ? (oq[q] + cb) | sb : oq[q] + cb;
+      const uint32_t off = (oq[q] + cb) | sb;
       v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0));
     }
   };
@@ -121,8 +123,8 @@ __global__ __launch_bounds__(64) void k_gram_mf_stream(GramStreamArgs G) {
     sum = 0.0;
   };
   // kGsRing-slot register ring, gathers kGsRing - 2 sub-batches ahead of the MFMAs (slots
-  // named statically: one ring turn per loop trip; past the range's end the gathers are
-  // padding ones, every offset outside the range)
+  // named statically: one ring turn per loop trip; past the range's end every offset carries
+  // the top bit, see rows())
   constexpr int AH = kGsRing - 2;
   float r[kGsRing][4];
 #pragma unroll

@@ -2234,312 +2234,7 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_grouped_mf(
   }
 }
 
-// ------------------------------------------------------------------------------------
-// MF k in {32, 64}, K_top <= 1: entity-shared scoring on the f64 matrix cores.
-// A work item is <= 256 ratings of one entity's list x <= 15 batch queries sharing the
-// entity (the same work items as k_score_grouped_mf, query blocks of 15).  Per 16-rating
-// tile the scores of every (query, rating) pair are one 16x16 tile
-//   D = X . G^T      (v_mfma_f64_16x16x4_f64, K/4 slices of 4 coordinates)
-// with A rows = the block's queries' x (side block, k coordinates) and row 15 = the
-// entity's own embedding, so D[15][n] = theta_e . g_n gives the rating's residual
-// e_n = r-hat_n - y_n without a VALU dot product.  Slice s pairs coordinate (K/4) kk + s
-// of lane group kk = l >> 4: every lane loads K/4 CONTIGUOUS coordinates of its query's
-// x (once per work item) and of its rating's gathered row (per tile, 16-B loads).
-// MI355X runs f64 MFMA and f64 VALU on the same units (tools/mb_f64.hip: their times
-// add), so the epilogue keeps f64 work per pair to 3 ops:
-//   influence = fma(e * (2/n), D + x_bias, c_q / n)      (mf:240-246)
-// Top-1 candidates: per lane and query a running best over its tiles (|v| bits as an
-// integer key), reduced over the 16 lanes of a query row once per work item.  D layout
-// (f64 16x16x4): lane l register r = D[(l >> 4) + 4 r][l & 15]; A[m][k] from lane
-// m + 16 k, B[k][n] from lane n + 16 k.
-// ------------------------------------------------------------------------------------
-constexpr int kMfmaRing = 3;   // tiles in flight (a fourth slot spills at 2 waves per SIMD: 3.26 vs 3.12 ms)
-
-// output stores of k_score_mf_mfma: 128-B runs of one query per 16 lanes, at the query's
-// arbitrary 8-B alignment; plain stores keep the straddled L2 lines until the next tile
-// completes them
-template <class T>
-__device__ __forceinline__ void st_out(T v, T* p) {
-  *p = v;
-}
-
-// every lane gets lane 48 + (l & 15)'s value (row 3 of a 16x16 f64 MFMA C register, column
-// l & 15): two permlane swaps and selects, no LDS round trip (a ds_bpermute waits ~100+
-// cycles right after the MFMA chain)
-__device__ __forceinline__ double bcast_row3(double x) {
-  const long long b = __double_as_longlong(x);
-  const unsigned lo = (unsigned)(b & 0xffffffffll), hi = (unsigned)(b >> 32);
-  // permlane32_swap(x, x) -> {[r0 r1 r0 r1], [r2 r3 r2 r3]} (rows of 16 lanes)
-  const auto l32 = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-  const auto h32 = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-  // permlane16_swap(y, y), y = [r2 r3 r2 r3] -> {[r2 r2 r2 r2], [r3 r3 r3 r3]}
-  const auto l16 = __builtin_amdgcn_permlane16_swap(l32[1], l32[1], false, false);
-  const auto h16 = __builtin_amdgcn_permlane16_swap(h32[1], h32[1], false, false);
-  return __longlong_as_double(((long long)h16[1] << 32) | l16[1]);
-}
-
-template <int CTRL>
-__device__ __forceinline__ void ikey_dpp_step(long long& k, int& p, double& v) {
-  const long long vb = __double_as_longlong(v);
-  const int klo = dpp_i32<CTRL>((int)(k & 0xffffffffll)), khi = dpp_i32<CTRL>((int)(k >> 32));
-  const int vlo = dpp_i32<CTRL>((int)(vb & 0xffffffffll)), vhi = dpp_i32<CTRL>((int)(vb >> 32));
-  const int p2 = dpp_i32<CTRL>(p);
-  const long long k2 = ((long long)khi << 32) | (unsigned)klo;
-  if (k2 > k || (k2 == k && p2 < p)) {
-    k = k2;
-    p = p2;
-    v = __longlong_as_double(((long long)vhi << 32) | (unsigned)vlo);
-  }
-}
-
-__device__ __forceinline__ long long topk_ikey(double v) {
-  // |v|'s bits order like |v| (non-negative doubles); NaN ranks below every number
-  const long long b = __double_as_longlong(v) & 0x7fffffffffffffffll;
-  return b > 0x7ff0000000000000ll ? -1ll : b;
-}
-
-template <class M, bool FULL>
-__global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_score_mf_mfma(
-    QueryArgs A, int64_t nE, const int64_t* __restrict__ wstart, const int32_t* __restrict__ witems,
-    const int64_t* __restrict__ gstart, const int32_t* __restrict__ gq, const int64_t* __restrict__ qbase,
-    const double* __restrict__ rec, int32_t* __restrict__ rel_idx, double* __restrict__ influence, int K_top,
-    int32_t* __restrict__ cand_pos, double* __restrict__ cand_val) {
-  constexpr int CPI = kMfmaCPI;
-  static_assert(!M::ncf && (M::K == 32 || M::K == 64), "MF k in {32, 64}");
-  constexpr int K = M::K, KS = K / 4, NF4 = KS / 4, TPC = kChunk / 16;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int kk = lane >> 4, cn = lane & 15;     // k-group; A row / B column / D column
-  const int64_t n_items = wstart[nE];
-  const int64_t stride = (int64_t)gridDim.x * (kScoreThreads / 64);
-  const double gbias = (double)A.t[4][0];
-  for (int64_t wi = (int64_t)blockIdx.x * (kScoreThreads / 64) + wave; wi < n_items; wi += stride) {
-    // work item: CPI consecutive chunks (cg) of the entity's list x one query block
-    const int32_t g = witems[3 * wi], cg = witems[3 * wi + 1], qblk = witems[3 * wi + 2];
-    const int64_t p0 = (int64_t)cg * (CPI * kChunk);   // first list position of the item
-    const int sd = g >= A.U ? 1 : 0;
-    const int32_t e = sd ? (int32_t)(g - A.U) : g;
-    const int64_t lb = A.ptr[sd][e] + p0;
-    const int64_t rem = A.ptr[sd][e + 1] - lb;
-    const int len = rem < CPI * kChunk ? (int)rem : CPI * kChunk;
-    const int64_t gb = gstart[g] + (int64_t)qblk * kMfmaQB;
-    const int64_t gn = gstart[g + 1] - gb;
-    const int nq = gn < kMfmaQB ? (int)gn : kMfmaQB;
-    const int32_t* __restrict__ oth = A.other[sd] + lb;
-    const float* __restrict__ rat = A.rating[sd] + lb;
-    const int32_t* __restrict__ rw = A.row[sd] + lb;
-    const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];     // the other side's table
-    const float* __restrict__ bt = sd == 0 ? A.t[3] : A.t[2];
-    const float* __restrict__ Es = sd == 0 ? A.t[0] : A.t[1];    // this side's (the entity's) table
-    const double bself = (double)(sd == 0 ? A.t[2] : A.t[3])[e];
-    // A operand: lane (row cn, group kk) holds coordinates KS*kk .. KS*kk+KS-1 of its row
-    double a[KS];
-    if (cn == 15) {
-      const float4* src = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
-#pragma unroll
-      for (int f = 0; f < NF4; ++f) {
-        const float4 t = src[f];
-        a[4 * f] = t.x; a[4 * f + 1] = t.y; a[4 * f + 2] = t.z; a[4 * f + 3] = t.w;
-      }
-    } else {
-      const int32_t q = gq[gb + (cn < nq ? cn : nq - 1)];
-      const double2* src = reinterpret_cast<const double2*>(rec + (int64_t)q * M::R + 4 + sd * M::SB + K + KS * kk);
-#pragma unroll
-      for (int f = 0; f < KS / 2; ++f) {
-        const double2 t = src[f];
-        a[2 * f] = t.x; a[2 * f + 1] = t.y;
-      }
-    }
-    // per D row r (query m = kk + 4 r): influence = fma(e * al, D + xb, be) at outp[r][p]
-    double al[4], be[4], xb[4];
-    double* outp[4];
-    int32_t* relp[4];
-    int32_t dupo[4], cpos[4];
-    int dl[4] = {0, 0, 0, 0};         // misalignment of each query row's output run (elements)
-    int64_t cslot[4];
-    bool qv[4];
-    {
-      // every query index first, then every per-query load (one wait)
-      int32_t qr[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = kk + 4 * r;
-        qv[r] = m < nq;
-        qr[r] = gq[gb + (m < nq ? m : 0)];
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double* __restrict__ R = rec + (int64_t)qr[r] * M::R;
-        const double inv_n = R[0];
-        al[r] = 2.0 * inv_n;
-        be[r] = R[1] * inv_n;
-        xb[r] = R[4 + sd * M::SB + 2 * K + 1];
-        const int32_t dup_other = (int32_t)R[4 + sd * M::SB + 2 * K + 2];
-        dupo[r] = qv[r] ? dup_other : -1;
-        const longlong2* __restrict__ qb = reinterpret_cast<const longlong2*>(qbase + 4 * (int64_t)qr[r]);
-        const longlong2 q01 = qb[0], q23 = qb[1];          // {out base user, item}, {slot base user, item}
-        const int64_t ob = (sd ? q01.y : q01.x) + p0 + cn;
-        cslot[r] = (sd ? q23.y : q23.x) + (int64_t)cg * CPI;
-        cpos[r] = (int32_t)(p0 + sd * (q01.y - q01.x));
-        // aligned stores: the run starts dl elements into a 16-element (128-B influence,
-        // 64-B train-row) segment; lane cn stores segment element cn
-        dl[r] = (int)((ob - cn) & 15);
-        outp[r] = influence + (ob - cn - dl[r]);   // the aligned segment (lane cn adds cn)
-        relp[r] = rel_idx + (ob - cn - dl[r]);
-      }
-    }
-    long long bk[4];
-    int bp[4];
-    double bv[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { bk[r] = -2; bp[r] = 0x7fffffff; bv[r] = 0.0; }
-    double prv[4] = {0.0, 0.0, 0.0, 0.0};     // previous tile's rotated values (aligned stores)
-    int32_t prw[4] = {0, 0, 0, 0};
-    const int ntl = (len + 15) / 16;
-    // software pipeline over the tiles, ring of three slots: the list entries of tile t + 2
-    // and the gathered rows of tile t + 1 are in flight while tile t is scored.  Positions
-    // past the chunk are clamped to its last entry (harmless loads, no branches).
-    int32_t so[kMfmaRing], sw[kMfmaRing];
-    float sy[kMfmaRing], sbo[kMfmaRing];
-    float4 sb[kMfmaRing][NF4];
-    auto load_list = [&](int t, int k3) {
-      const int p = 16 * t + cn < len ? 16 * t + cn : len - 1;
-      so[k3] = oth[p];
-      sy[k3] = rat[p];
-      sw[k3] = rw[p];
-    };
-    auto gather = [&](int k3) {
-      const float4* row = reinterpret_cast<const float4*>(T + (int64_t)so[k3] * K + KS * kk);
-#pragma unroll
-      for (int f = 0; f < NF4; ++f) sb[k3][f] = row[f];
-      sbo[k3] = bt[so[k3]];
-    };
-    // per chunk (16 tiles): best of each query row over the row's 16 lanes (xor 1..8 stays
-    // inside the row) -> the chunk's candidate slot; then the running bests restart
-    auto emit = [&](int chunk) {
-      if (K_top <= 0) return;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        long long k1 = bk[r];
-        int p1 = bp[r];
-        double v1 = bv[r];
-        // the row's best over its 16 lanes by DPP row rotations (order-independent: strict
-        // (key, position) order, unique positions)
-        ikey_dpp_step<0x128>(k1, p1, v1);
-        ikey_dpp_step<0x124>(k1, p1, v1);
-        ikey_dpp_step<0x122>(k1, p1, v1);
-        ikey_dpp_step<0x121>(k1, p1, v1);
-        if (cn == 0 && qv[r]) {       // (no loads here: a load in the tile loop drains vmcnt)
-          const int64_t slot = (cslot[r] + chunk) * K_top;
-          const bool okk = k1 > -2;
-          cand_pos[slot] = okk ? (int32_t)(cpos[r] + p1) : -1;
-          cand_val[slot] = okk ? v1 : NAN;
-        }
-        bk[r] = -2; bp[r] = 0x7fffffff; bv[r] = 0.0;
-      }
-    };
-    auto tile = [&](int t, int k3) {
-      // the whole tile's B operands converted first: f64 VALU and f64 MFMA share the
-      // MI355X's double-precision units (tools/mb_f64.hip), so a conversion slotted between
-      // two MFMAs waits for the first to drain; the empty asm pins them before the chain
-      double bd[KS];
-#pragma unroll
-      for (int f = 0; f < NF4; ++f) {
-        bd[4 * f] = sb[k3][f].x; bd[4 * f + 1] = sb[k3][f].y; bd[4 * f + 2] = sb[k3][f].z; bd[4 * f + 3] = sb[k3][f].w;
-      }
-      if constexpr (KS == 16)
-        asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
-                     "+v"(bd[6]), "+v"(bd[7]), "+v"(bd[8]), "+v"(bd[9]), "+v"(bd[10]), "+v"(bd[11]),
-                     "+v"(bd[12]), "+v"(bd[13]), "+v"(bd[14]), "+v"(bd[15]));
-      else
-        asm volatile("" : "+v"(bd[0]), "+v"(bd[1]), "+v"(bd[2]), "+v"(bd[3]), "+v"(bd[4]), "+v"(bd[5]),
-                     "+v"(bd[6]), "+v"(bd[7]));
-      d4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int sl = 0; sl < KS; ++sl) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[sl], bd[sl], acc, 0, 0, 0);
-      const int p = 16 * t + cn;                // position in the chunk of this lane's rating
-      const bool pv = p < len;
-      const int32_t o = so[k3], w = sw[k3];
-      const double y = (double)sy[k3];
-      // residual of rating cn: D[15][cn] lives in lane 48 + cn, register 3
-      const double dself = bcast_row3(acc[3]);
-      const double en = ((dself + bself) + (double)sbo[k3]) + gbias - y;
-      const bool dup = pv && (o == dupo[0] || o == dupo[1] || o == dupo[2] || o == dupo[3]);
-      double val[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) val[r] = fma(en * al[r], acc[r] + xb[r], be[r]);
-      if (__builtin_expect(__ballot(dup) != 0, 0)) {
-        // the test pair's own train row: e = r-hat(u,i) - y, s = x . v (as in k_solve)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (!(pv && qv[r] && o == dupo[r])) continue;
-          const int32_t q = gq[gb + kk + 4 * r];
-          const double* __restrict__ R = rec + (int64_t)q * M::R;
-          val[r] = fma((R[3] - y) * al[r], R[2], be[r]);
-        }
-      }
-      // rotate each row by its misalignment dl: lane cn takes element (cn - dl) & 15 -- of
-      // this tile (cn >= dl) or, already rotated, of the previous tile (cn < dl) -- so each
-      // store is one aligned 16-element segment (whole lines: no line written twice).  All
-      // twelve cross-lane reads are issued before the first store: one LDS wait per tile
-      // instead of one per row
-      double rv[4];
-      int32_t rw[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int srcl = ((cn - dl[r]) & 15) + 16 * kk;
-        rv[r] = __shfl(val[r], srcl);
-        rw[r] = __shfl(w, srcl);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool ok = pv && qv[r];
-        const long long key = ok ? topk_ikey(val[r]) : -2ll;
-        const bool take = key > bk[r];
-        bk[r] = take ? key : bk[r];
-        bp[r] = take ? p : bp[r];
-        bv[r] = take ? val[r] : bv[r];
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool cur = cn >= dl[r];
-        const int idx = 16 * t + cn - dl[r];          // element of the run this lane stores
-        if (qv[r] && (cur ? idx < len : t > 0)) {
-          if (FULL || influence) st_out(cur ? rv[r] : prv[r], outp[r] + 16 * t + cn);
-          if (FULL || rel_idx) st_out(cur ? rw[r] : prw[r], relp[r] + 16 * t + cn);
-        }
-        prv[r] = rv[r];
-        prw[r] = rw[r];
-      }
-      if (t % TPC == TPC - 1 || t == ntl - 1) emit(t / TPC);
-    };
-    load_list(0, 0);
-    load_list(1, 1);
-    gather(0);
-    for (int t = 0; t < ntl; t += 3) {
-      load_list(t + 2, 2);
-      gather(1);
-      tile(t, 0);
-      if (t + 1 >= ntl) break;
-      load_list(t + 3, 0);
-      gather(2);
-      tile(t + 1, 1);
-      if (t + 2 >= ntl) break;
-      load_list(t + 4, 1);
-      gather(0);
-      tile(t + 2, 2);
-    }
-    // the run's tail: the last tile's elements past the last aligned segment
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int idx = 16 * ntl + cn - dl[r];
-      if (qv[r] && cn < dl[r] && idx < len) {
-        if (FULL || influence) st_out(prv[r], outp[r] + 16 * ntl + cn);
-        if (FULL || rel_idx) st_out(prw[r], relp[r] + 16 * ntl + cn);
-      }
-    }
-  }
-}
+// MF k in {32, 64}, K_top <= 1: k_score_mf_mfma (score_mfma.hip)
 
 // NCF k <= 16 (mask path): T[m][c] = sum_e W2[c][e] W3m[e] [bit e of m], the d1 of a train
 // row whose z2 ReLU mask is m (before its z1 mask), one thread per entry
@@ -2982,16 +2677,20 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
     }
   }
   constexpr int GSP = (GS + 1) & ~1;
+  // the slice lists of the per-slice Gram kernels (k_ncf_gram_rows, k_gram_mf_mfma); the MF
+  // k <= 16 Gram stream cuts its own sub-batches (build_gram_stream) and needs neither these
+  // lists nor their partial-Gram slots
+  const bool stream = use_gram_stream<M>(n_ent);
   // Gram slice length: short slices for parallelism, long enough that the partial Grams
   // of split lists (GSP doubles each) stay a few bytes per rating (MI355X: ml-1m-ex MF k=16
   // best at 256, 20M MF k=64 loses 30% at 256 vs 512)
-  {
+  if (!stream) {
     int64_t want = 256;
     while (!M::ncf && want < 4096 && want < GSP) want *= 2;   // NCF: 256 (16 slabs per item)
     if (c->idx.gchunk != want) FIA_HIP_TRY(build_gram_lists(c, want, s));
   }
   const Index& X = c->idx;
-  for (int sd = 0; sd < 2; ++sd)
+  for (int sd = 0; sd < 2 && !stream; ++sd)
     if (X.n_gslots[sd] > 0) FIA_HIP_TRY(c->gpart[sd].reserve(sizeof(double) * (size_t)(X.n_gslots[sd] * GSP), s));
   GramSides G{};
   for (int sd = 0; sd < 2; ++sd) {
@@ -3027,7 +2726,7 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
                          X.side[0].rating.as<float>(), X.side[1].rating.as<float>(), c->resid.as<double>());
       FIA_HIP_TRY(hipGetLastError());
     }
-  } else if (use_gram_stream<M>(n_ent)) {
+  } else if (stream) {
     // MF k <= 16: the Gram stream (both sides, one launch), then the partial slices combined
     FIA_HIP_TRY(build_gram_stream(c, K, s));
     for (int sd = 0; sd < 2; ++sd)
@@ -3076,15 +2775,15 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                       int64_t max_chunks, int32_t* rel_idx, double* influence, double* x_out, int K,
                       int64_t* topk_pos, int64_t* topk_idx, double* topk_val, hipStream_t s,
                       const double* x_in) {
-  // One scoring schedule per (model, k, K) (measured on MI355X, profiles/): MF k <= 16 item
-  // runs (k_score_mf_runs, per-query chunks sharing the item's list); MF k in {32, 64}
-  // entity-shared, on f64 MFMA for K <= 1 (k_score_mf_mfma, query blocks of 15) and on VALU
-  // otherwise (k_score_grouped_mf); NCF entity-shared (k_score_ncf)
-  // item runs: MF k <= 16 (k_score_mf_runs) and NCF k <= 16 (k_score_ncf_runs)
+  // One scoring schedule per (model, k, K) (measured on MI355X, profiles/): k <= 16 item runs
+  // (MF k_score_mf_runs, NCF k_score_ncf_runs: per-query chunks sharing the item's list); MF
+  // k in {32, 64} entity-shared, on f64 MFMA for K <= 1 (k_score_mf_mfma, query blocks of 15)
+  // and on VALU otherwise (k_score_grouped_mf); NCF k = 32 entity-shared (k_score_ncf)
   constexpr bool grouped = M::ncf ? !mask_path<M>() : M::K >= 32;
   constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);
   const bool use_mfma = mfma_ok && K <= 1;
-  const int qblock = use_mfma ? kMfmaQB : query_block<M>();
+  // (the MFMA kernel's work item is a group of kWgBlocks query blocks, one per wave)
+  const int qblock = use_mfma ? kMfmaQB * kWgBlocks : query_block<M>();
   constexpr bool runs = !grouped;
   constexpr int spc = 1;      // candidate slot sets per chunk
   static_assert(solve_covered<M>(), "every small-k model has a side-system solve");
@@ -3190,6 +2889,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   const int64_t gcap = M::ncf ? 1024 : 8192;
   if (grid > gcap) grid = gcap;
   if (runs) grid = runs_grid;
+  // the MFMA kernel: one work item per workgroup (grid-stride)
+  if (use_mfma) grid = max_items < 8192 ? (max_items > 0 ? max_items : 1) : 8192;
   const PhaseSpan span = phase_span(c, 2);
   if (grouped) {
     if constexpr (M::ncf)
@@ -3200,12 +2901,10 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     else {
       if constexpr (mfma_ok) {
         if (use_mfma) {
-          auto kern = rel_idx && influence ? k_score_mf_mfma<M, true> : k_score_mf_mfma<M, false>;
-          hipExtLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kScoreThreads), 0, s, span.a, span.b, 0, A, nE,
-                                c->wstart.as<int64_t>(), c->witems.as<int32_t>(), c->gstart.as<int64_t>(),
-                                c->gq.as<int32_t>(), c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence,
-                                K, c->cand_pos.as<int32_t>(), c->cand_val.as<double>());
-          FIA_HIP_TRY(hipGetLastError());
+          FIA_HIP_TRY(launch_score_mf_mfma(M::K, rel_idx && influence, grid, s, span, A, nE, c->wstart.as<int64_t>(),
+                                           c->witems.as<int32_t>(), c->gstart.as<int64_t>(), c->gq.as<int32_t>(),
+                                           c->qbase.as<int64_t>(), c->rec.as<double>(), rel_idx, influence, K,
+                                           c->cand_pos.as<int32_t>(), c->cand_val.as<double>()));
           goto topk;
         }
       }

@@ -96,6 +96,7 @@ class Context(object):
         self._keep = []
         self._mask = 0
         self._carry = None      # phase sums drained by profiled_call on the caller's behalf
+        self.full_prepared = False   # every entity's caches (the last prepare was fia_prepare)
 
     def close(self):
         if getattr(self, "h", None):
@@ -118,20 +119,25 @@ class Context(object):
         """tables: list of contiguous float32 cuda tensors in include/fia.h order."""
         arr = (ctypes.c_void_p * len(tables))(*[t.data_ptr() for t in tables])
         self._keep = list(tables)
+        self.full_prepared = False
         rc = self.lib.fia_set_params(self.h, model, k, U, I, arr, len(tables), float(wd), float(damping))
         self._check(rc, "fia_set_params")
 
     def build_index(self, users, items, ratings, U, I):
+        self.full_prepared = False
         rc = self.lib.fia_build_index(self.h, users.numel(), U, I, _ptr(users), _ptr(items), _ptr(ratings),
                                       _stream())
         self._check(rc, "fia_build_index")
 
     def prepare(self):
+        self.full_prepared = False
         self._check(self.lib.fia_prepare(self.h, _stream()), "fia_prepare")
+        self.full_prepared = True
 
     def prepare_for(self, qu, qi):
         """Hessian caches for only the users/items of these queries (fia_prepare_for, every
         model: small k marks the entities on the device, large k builds a compact cache)."""
+        self.full_prepared = False
         self._check(self.lib.fia_prepare_for(self.h, qu.numel(), _ptr(qu), _ptr(qi), _stream()), "fia_prepare_for")
 
     def num_params(self):

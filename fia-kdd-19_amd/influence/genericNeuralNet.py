@@ -311,6 +311,9 @@ class GenericNeuralNet(object):
         self._train_ratings = torch.from_numpy(np.ascontiguousarray(train.labels, np.float32)).to(dev)
         self.ctx.build_index(self._train_users, self._train_items, self._train_ratings, self.num_users,
                              self.num_items)
+        # host degree counts: a single query's related-set size without a count round trip
+        self._deg_u = np.bincount(np.asarray(users, np.int64), minlength=self.num_users)
+        self._deg_i = np.bincount(np.asarray(items, np.int64), minlength=self.num_items)
 
     # --------------------------------------------------------------- queries
     def _test_pair(self, test_index):
@@ -442,8 +445,7 @@ class GenericNeuralNet(object):
                 print(("Loaded inverse HVP from %s" if cached is not None else
                        "Ignored unusable inverse HVP file %s") % fname)
         # (the caller's own profiling mask and unread sums are kept: Context.profiled_call)
-        res, phases = self.ctx.profiled_call(
-            lambda: self.get_influence_batch(test_indices, K=0, full=True, return_x=True, inverse_hvp=cached))
+        res, phases = self.ctx.profiled_call(lambda: self._one_query(self.test_index, cached))
         self.train_indices_of_test_case = res["rel_idx"]
         x = res["x"][0]
         self.num_params = x.size
@@ -453,6 +455,56 @@ class GenericNeuralNet(object):
         self.last_timing = rq2_timing(phases, res["influence"].size, time.time() - t0,
                                       log=print if self.verbose else None)
         return res["influence"]
+
+    def _one_query(self, test_index, inverse_hvp=None):
+        """One test rating, as get_influence_batch([test_index], K=0) returns it, with a single
+        host synchronisation (the reference times each query, RQ2.py:53,57): the related-set size
+        from host degree counts instead of a count round trip, persistent device and pinned host
+        buffers, the query pair and every result copied in stream order, one wait at the end.
+        Falls back to get_influence_batch when its checks are needed: ids out of range (the
+        count raises) or caches built by prepare_for (the cover check raises)."""
+        import torch
+        u, i = self._test_pair(test_index)
+        if not (0 <= u < self.num_users and 0 <= i < self.num_items) or not self.ctx.full_prepared:
+            return self.get_influence_batch([test_index], K=0, full=True, return_x=True, inverse_hvp=inverse_hvp)
+        n = int(self._deg_u[u] + self._deg_i[i])
+        D = self.ctx.num_params()
+        dev = self.ctx.torch_device
+        b = getattr(self, "_one_bufs", None)
+        if b is None or b["cap"] < max(n, 1) or b["D"] != D:
+            cap = max(n, 1024, 2 * (b["cap"] if b else 0))
+            b = dict(cap=cap, D=D,
+                     q=torch.empty(2, dtype=torch.int32, device=dev),
+                     off=torch.empty(2, dtype=torch.int64, device=dev),
+                     rel=torch.empty(cap, dtype=torch.int32, device=dev),
+                     infl=torch.empty(cap, dtype=torch.float64, device=dev),
+                     x=torch.empty(D, dtype=torch.float64, device=dev),
+                     hq=torch.empty(2, dtype=torch.int32, pin_memory=True),
+                     hoff=torch.empty(2, dtype=torch.int64, pin_memory=True),
+                     hrel=torch.empty(cap, dtype=torch.int32, pin_memory=True),
+                     hinfl=torch.empty(cap, dtype=torch.float64, pin_memory=True),
+                     hx=torch.empty(D, dtype=torch.float64, pin_memory=True))
+            self._one_bufs = b
+        b["hq"].numpy()[:] = (u, i)
+        b["q"].copy_(b["hq"], non_blocking=True)
+        qu, qi = b["q"][0:1], b["q"][1:2]
+        self.ctx.count_related(qu, qi, b["off"], want_total=False)
+        if inverse_hvp is not None:
+            xin = np.ascontiguousarray(np.asarray(inverse_hvp, np.float64).reshape(-1))
+            if xin.size != D:
+                raise ValueError("inverse_hvp must hold %d values" % D)
+            b["hx"].numpy()[:] = xin
+            b["x"].copy_(b["hx"], non_blocking=True)
+            self.ctx.query_batch_x(qu, qi, b["off"], n, b["x"], b["rel"], b["infl"], 0, None, None, None)
+        else:
+            self.ctx.query_batch(qu, qi, b["off"], n, b["rel"], b["infl"], b["x"], 0, None, None, None)
+        b["hoff"].copy_(b["off"], non_blocking=True)
+        b["hrel"][:n].copy_(b["rel"][:n], non_blocking=True)
+        b["hinfl"][:n].copy_(b["infl"][:n], non_blocking=True)
+        b["hx"].copy_(b["x"], non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        return dict(offsets=b["hoff"].numpy().copy(), rel_idx=b["hrel"][:n].numpy().astype(np.int64),
+                    influence=b["hinfl"][:n].numpy().copy(), x=b["hx"].numpy().copy().reshape(1, D))
 
     def _split_theta(self, x):
         raise NotImplementedError

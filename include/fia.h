@@ -29,7 +29,11 @@
  *     thread-safe; use one context per GPU / process.  A call on a new stream first
  *     synchronises the previous one -- except when the new stream is being captured
  *     into a HIP graph (no synchronisation is legal there): finish the previous
- *     stream's work (e.g. an eager warm-up) before the capture begins.
+ *     stream's work (e.g. an eager warm-up) before the capture begins.  An eager
+ *     fia_prepare / fia_prepare_for may run its Gram pass on the context's own aux
+ *     stream, joined by the next fia_query_batch / fia_prepare; a capture may only
+ *     start once that join has happened (the aux stream is idle to the capture):
+ *     otherwise the first call on the capturing stream returns FIA_ERR_STATE.
  *   - Every entry point returns FIA_OK (0) or an error code; no exception
  *     crosses the ABI.  fia_last_error() describes the last failure.
  *   - Ids are int32 in [0, num_users) / [0, num_items); ratings are float32.

@@ -2,8 +2,8 @@
 
   * config 4 -- synthetic 20M ratings, MF k=64: all 276,986 held-out queries in
     fia_query_batch batches (as bench.py runs them), every batch checked on the GPU;
-  * config 5 -- the same ratings, MF k=256 and NCF k=256: shards 0, 3 and 7 of the 8-GPU
-    split bench.py runs, caches from fia_prepare_for;
+  * config 5 -- the same ratings, MF k=256 and NCF k=256: all 8 shards of the 8-GPU split
+    bench.py runs, caches from fia_prepare_for;
   * config 3 -- yelp-ex NCF k=16: all 51,153 test ratings in one batch.
 
 Size-independent properties, checked for EVERY query with torch on the GPU (the
@@ -191,10 +191,10 @@ def test_config4_mf64_all_queries(data20m):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("shard", [0, 3, 7])
+@pytest.mark.parametrize("shard", range(8))
 @pytest.mark.parametrize("model", ["MF", "NCF"])
 def test_config5_k256_shard(data20m, model, shard):
-    """Config 5: k=256 (MF 2 x 257^2, NCF 2 x 512^2 blocks per query) on shards 0, 3 and 7 of
+    """Config 5: k=256 (MF 2 x 257^2, NCF 2 x 512^2 blocks per query) on every shard of
     the 8-GPU split bench.py runs (n_q + the config's per-query cost, shard_ranges), caches from
     fia_prepare_for; every batch checked on the GPU; an fp64 oracle sample of >= 16 queries per
     shard: the shard's heaviest query (no size cap: the heaviest of any shard has ~122 k related

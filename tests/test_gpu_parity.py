@@ -559,3 +559,144 @@ def test_graph_capture_matches_eager(model):
     for name in eager:
         a, b = eager[name].cpu().numpy(), rep[name].cpu().numpy()
         assert np.array_equal(a, b, equal_nan=True), name
+
+
+def test_graph_capture_refused_after_unjoined_prepare():
+    """An eager fia_prepare that forks its Gram pass onto the context's aux stream (NCF k=16)
+    followed directly by a capture: the captured kernels could not depend on that pass, so the
+    first call inside the capture fails with FIA_ERR_STATE (no host wait is legal there); after
+    a joining eager query the same capture succeeds and replays bit-identical to eager."""
+    import torch
+    from influence import _lib
+    rng = np.random.default_rng(78)
+    U, I, N, k = 300, 60, 5000, 16
+    key = np.sort(rng.choice(U * I, N, replace=False))
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, N).astype(np.float32)
+    p = synth.ncf_params(U, I, k, 8)
+    qi_np = np.sort(rng.integers(0, I, 200)).astype(np.int32)
+    qu_np = rng.integers(0, U, 200).astype(np.int32)
+    dev = torch.device("cuda:0")
+    ctx = _lib.Context(0)
+    tables = [torch.from_numpy(np.ascontiguousarray(p[n], np.float32)).to(dev) for n in p]
+    ctx.set_params(_lib.FIA_MODEL_NCF, k, U, I, tables, 1e-3, 1e-6)
+    ctx.build_index(torch.from_numpy(tu).to(dev), torch.from_numpy(ti).to(dev), torch.from_numpy(tr).to(dev), U, I)
+    qu, qi = torch.from_numpy(qu_np).to(dev), torch.from_numpy(qi_np).to(dev)
+    off, tot = ctx.count_related(qu, qi)
+    D, K, Q = ctx.num_params(), 2, qu_np.size
+
+    def bufs():
+        return dict(rel=torch.full((tot,), -7, dtype=torch.int32, device=dev),
+                    infl=torch.full((tot,), float("nan"), dtype=torch.float64, device=dev),
+                    x=torch.zeros(Q * D, dtype=torch.float64, device=dev),
+                    tp=torch.zeros(Q * K, dtype=torch.int64, device=dev),
+                    tix=torch.zeros(Q * K, dtype=torch.int64, device=dev),
+                    tv=torch.zeros(Q * K, dtype=torch.float64, device=dev))
+
+    def step(b):
+        ctx.prepare()
+        ctx.count_related(qu, qi, off, want_total=False)
+        ctx.query_batch(qu, qi, off, tot, b["rel"], b["infl"], b["x"], K, b["tp"], b["tix"], b["tv"])
+
+    eager = bufs()
+    step(eager)
+    torch.cuda.synchronize(dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        ctx.prepare()                        # forked, not joined by any query
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    refused = torch.cuda.CUDAGraph()
+    with pytest.raises(_lib.FIAError, match="not joined"):
+        with torch.cuda.graph(refused):
+            ctx.prepare()
+    del refused
+    rep = bufs()
+    with torch.cuda.stream(side):
+        step(rep)                            # the query joins the pending pass
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    for v in rep.values():
+        v.zero_()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step(rep)
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    for name in eager:
+        a, b = eager[name].cpu().numpy(), rep[name].cpu().numpy()
+        assert np.array_equal(a, b, equal_nan=True), name
+    ctx.close()
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_prepare_for_sliced_item_lists(k, tmp_path):
+    """MF k <= 16 fia_prepare_for with item lists longer than a Gram-stream slice (256
+    ratings): the marked entities' partial Grams of several slices are summed by
+    k_gram_combine; results equal the full prepare's bit for bit (matrix_factorization.py:
+    315-322: one Hessian per query whichever caches exist)."""
+    rng = np.random.default_rng(90 + k)
+    U, I, N = 3000, 24, 20000
+    # skewed items: a few hold > 1000 ratings (several 256-rating slices), most fewer
+    w = 1.0 / np.arange(1, I + 1) ** 1.2
+    items = rng.choice(I, N, p=w / w.sum())
+    users = rng.integers(0, U, N)
+    key = np.unique(users.astype(np.int64) * I + items)
+    tu, ti = (key // I).astype(np.int32), (key % I).astype(np.int32)
+    tr = rng.integers(1, 6, tu.size).astype(np.float32)
+    assert np.bincount(ti, minlength=I).max() > 1000
+    p = synth.mf_params(U, I, k, 6)
+    qu = rng.integers(0, U, 40).astype(np.int32)
+    qi = rng.integers(0, I, 40).astype(np.int32)
+    qi[:4] = np.argsort(-np.bincount(ti, minlength=I))[:4]      # the longest lists
+    m = make_model("MF", U, I, k, (tu, ti, tr), (qu, qi), p, tmpdir=tmp_path)
+    full = m.get_influence_batch(list(range(40)), K=2)
+    subset = list(range(0, 40, 2))
+    m.prepare_for(subset)
+    part = m.get_influence_batch(subset, K=2)
+    for j, q in enumerate(subset):
+        b, e = full["offsets"][q], full["offsets"][q + 1]
+        pb, pe = part["offsets"][j], part["offsets"][j + 1]
+        assert np.array_equal(part["rel_idx"][pb:pe], full["rel_idx"][b:e])
+        assert np.array_equal(part["influence"][pb:pe], full["influence"][b:e])
+        assert np.array_equal(part["x"][j], full["x"][q])
+    from oracle import fia_oracle as fo
+    for q in subset[:3]:
+        o = fo.query("MF", p, k, tu, ti, tr, int(qu[q]), int(qi[q]), 1e-3, 1e-6)
+        b, e = full["offsets"][q], full["offsets"][q + 1]
+        assert rel_err(full["influence"][b:e], o["influence"]) < RTOL
+
+
+@pytest.mark.parametrize("model", ["MF", "NCF"])
+def test_single_query_path_matches_batch(model, tmp_path):
+    """get_influence_on_test_loss's one-sync single-query path (host degree counts, persistent
+    pinned buffers) returns the batch path's bits for ml-1m-ex queries -- RQ2's test_idx 59,
+    the heaviest query, a train-pair query, growing related-set sizes (buffer regrowth) -- and
+    after prepare_for it takes the checked path (an uncovered query raises)."""
+    from influence._lib import FIAError
+    d = synth.make_dataset(synth.ML1M, seed=0)
+    tu, ti, tr = d["train"]
+    qu, qi, _ = d["test"]
+    p = (synth.mf_params if model == "MF" else synth.ncf_params)(d["U"], d["I"], 16, 0)
+    qu = np.append(qu, np.int32(tu[5]))           # a train pair (coupled system)
+    qi = np.append(qi, np.int32(ti[5]))
+    m = make_model(model, d["U"], d["I"], 16, d["train"], (qu, qi), p, tmpdir=tmp_path)
+    m.save_inverse_hvp = False
+    n = np.bincount(tu, minlength=d["U"])[qu] + np.bincount(ti, minlength=d["I"])[qi]
+    order = [int(j) for j in np.argsort(n)[::1200]]
+    qs = [59, int(np.argmax(n)), qu.size - 1] + order
+    for t in qs:
+        one = m.get_influence_on_test_loss([t], np.arange(tu.size))
+        ref = m.get_influence_batch([t], K=0)
+        assert np.array_equal(m.train_indices_of_test_case, ref["rel_idx"])
+        assert np.array_equal(one.view(np.int64), ref["influence"].view(np.int64)), t
+        x = np.concatenate([np.ravel(a) for a in m.inverse_hvp])
+        assert np.array_equal(x.view(np.int64), ref["x"][0].view(np.int64)), t
+    m.prepare_for([0, 1])
+    far = next(t for t in range(qu.size) if qu[t] not in qu[:2] and qi[t] not in qi[:2])
+    with pytest.raises(FIAError):
+        m.get_influence_on_test_loss([far], np.arange(tu.size))
+    m.ctx.prepare()
+    again = m.get_influence_on_test_loss([far], np.arange(tu.size))
+    assert np.array_equal(again.view(np.int64), m.get_influence_batch([far], K=0)["influence"].view(np.int64))
