@@ -20,7 +20,14 @@ from the environment.  Scaling (`--scaling`; every config defaults to strong):
     workload's own pairs, rank r > 0 the same users and item multiset re-paired by
     a seeded permutation (distinct pairs, none a training row).
 The only exchange is the RCCL all_gather of the per-query top-K lists, overlapped
-with the next step.  `value` = queries answered by all ranks / the max-over-ranks
+with the next step.
+
+Batches in flight (`--inflight L`, default 2 for the sub-ms ml-1m-ex / yelp-ex steps): the
+steps alternate over L library contexts, each with its own index, caches, scratch and output
+buffers, each on its own HIP stream -- a serving pipeline's two query batches in flight, so
+one step's kernel ramps and tails overlap the next step's kernels.  Every timed step still
+runs the whole hot path over the whole batch; the timed region is still K steps between two
+synchronisations.  `value` = queries answered by all ranks / the max-over-ranks
 time of the timed steps.
 
 Rank 0 prints one JSON line.  `roofline` prices the step's dominant phase (from a few
@@ -56,9 +63,9 @@ FP64_PEAK_TFS = 78.6       # MI355X dense FP64 (vector and matrix; tools/mb_f64.
 # query over 6.0 ps per scored rating
 CONFIGS = {
     "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m",
-                    scaling="strong", query_cost=560),
+                    scaling="strong", query_cost=560, inflight=2),
     "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp",
-                     scaling="strong", query_cost=210),
+                     scaling="strong", query_cost=210, inflight=2),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
                      k=64, data="20m", scaling="strong", query_cost=10100),
     "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "
@@ -87,6 +94,11 @@ def parse(argv=None):
                          "of the 8-GPU job)")
     ap.add_argument("--shard-index", type=int, default=0,
                     help="with --shard-of S at N=1: which shard (0 .. S-1) to answer")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="query batches in flight: steps alternate over this many contexts, each on its own "
+                         "stream with its own caches and outputs, so one step's kernel ramp and tail overlap "
+                         "the next step's kernels (every step still runs the whole hot path); 0 = the config's "
+                         "default (2 for the sub-ms ml-1m-ex / yelp-ex steps, else 1)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one captured HIP graph (measured no faster on MI355X)")
     ap.add_argument("--no-timed-events", action="store_true",
@@ -560,12 +572,30 @@ def main():
         batches.append((b0, b1, qb_u, qb_i, off_b, tot_b))
     max_rows = max([b[5] for b in batches] + [1])
     max_q = max([b[1] - b[0] for b in batches] + [1])
-    rel = torch.empty(max_rows, dtype=torch.int32, device=dev)
-    infl = torch.empty(max_rows, dtype=torch.float64, device=dev)
-    xbuf = torch.empty(max_q * D, dtype=torch.float64, device=dev)
-    tp = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev)
-    tix = torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev)
-    tv = torch.empty(max(Q * K, 1), dtype=torch.float64, device=dev)
+
+    def lane_state(c, bat):
+        return dict(ctx=c, batches=bat,
+                    rel=torch.empty(max_rows, dtype=torch.int32, device=dev),
+                    infl=torch.empty(max_rows, dtype=torch.float64, device=dev),
+                    xbuf=torch.empty(max_q * D, dtype=torch.float64, device=dev),
+                    tp=torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev),
+                    tix=torch.empty(max(Q * K, 1), dtype=torch.int64, device=dev),
+                    tv=torch.empty(max(Q * K, 1), dtype=torch.float64, device=dev))
+
+    # --inflight L: L contexts (own index, caches, scratch and outputs) on L streams
+    lanes = [lane_state(ctx, batches)]
+    streams = [torch.cuda.current_stream(dev)]
+    n_inflight = args.inflight if args.inflight > 0 else cfg.get("inflight", 1)
+    for _ in range(1, max(1, n_inflight)):
+        c2 = _lib.Context(dev.index)
+        c2.set_params(model_id, k, U, I, tables, 1e-3, 1e-6)
+        c2.build_index(t_u, t_i, t_r, U, I)
+        bat2 = [(b0, b1, qb_u, qb_i, c2.count_related(qb_u, qb_i)[0], tot_b)
+                for b0, b1, qb_u, qb_i, _, tot_b in batches]
+        lanes.append(lane_state(c2, bat2))
+        streams.append(torch.cuda.Stream(device=dev))
+    torch.cuda.synchronize(dev)
+    rel, infl, xbuf, tp, tix, tv = (lanes[0][n] for n in ("rel", "infl", "xbuf", "tp", "tix", "tv"))
 
     big_k = k >= 128 or (cfg["model"] == "NCF" and k >= 64)
 
@@ -578,19 +608,32 @@ def main():
     # (fia_prepare_for; small k: marked on the device, no host round trip); the full set
     # builds every cache
     sharded = shard_of > 1
-    def compute():
-        if big_k or sharded:
-            ctx.prepare_for(qu, qi)
-        else:
-            ctx.prepare()
-        for b0, b1, qb_u, qb_i, off_b, tot_b in batches:
-            ctx.count_related(qb_u, qb_i, off_b, want_total=False)
-            ctx.query_batch(qb_u, qb_i, off_b, tot_b, rel, infl, xbuf, K, tp[b0 * K:b1 * K],
-                            tix[b0 * K:b1 * K], tv[b0 * K:b1 * K])
+    step_no = [0]
 
-    def exchange():
+    def compute_lane(L):
+        c = L["ctx"]
+        if big_k or sharded:
+            c.prepare_for(qu, qi)
+        else:
+            c.prepare()
+        for b0, b1, qb_u, qb_i, off_b, tot_b in L["batches"]:
+            c.count_related(qb_u, qb_i, off_b, want_total=False)
+            c.query_batch(qb_u, qb_i, off_b, tot_b, L["rel"], L["infl"], L["xbuf"], K, L["tp"][b0 * K:b1 * K],
+                          L["tix"][b0 * K:b1 * K], L["tv"][b0 * K:b1 * K])
+
+    def compute():
+        j = step_no[0] % len(lanes)
+        step_no[0] += 1
+        if j == 0:
+            compute_lane(lanes[0])
+        else:
+            with torch.cuda.stream(streams[j]):
+                compute_lane(lanes[j])
+        return j
+
+    def exchange(j=0):
         if tg is not None:
-            a, b = tix[:Q * K].view(Q, K), tv[:Q * K].view(Q, K)
+            a, b = lanes[j]["tix"][:Q * K].view(Q, K), lanes[j]["tv"][:Q * K].view(Q, K)
             if gdev.type == "cpu":
                 a, b = a.cpu(), b.cpu()
             tg.start(a, b)
@@ -603,25 +646,35 @@ def main():
         torch.cuda.synchronize(dev)
         n_spin += 1
     for _ in range(args.warmup):
-        compute()
-        exchange()
+        exchange(compute())
     if tg is not None:
         tg.wait()
     torch.cuda.synchronize(dev)
     # per-phase breakdown (informational) from a few instrumented steps; the timed steps
     # below record only the scoring phase's event pair (the roofline kernel time)
-    ctx.profile_read()
-    ctx.set_profiling(True)
+    def read_all():
+        tot = {}
+        for L in lanes:
+            for p, v in L["ctx"].profile_read().items():
+                a = tot.get(p, (0.0, 0))
+                tot[p] = (a[0] + v[0], a[1] + v[1])
+        return tot
+
+    read_all()
+    for L in lanes:
+        L["ctx"].set_profiling(True)
+    # (instrumented steps one at a time: the per-phase breakdown of an un-overlapped step)
     n_instr = max(1, min(args.steps, 5))
     for _ in range(n_instr):
         compute()
-    torch.cuda.synchronize(dev)
-    ctx.set_profiling(False)
-    phases = ctx.profile_read()
+        torch.cuda.synchronize(dev)
+    for L in lanes:
+        L["ctx"].set_profiling(False)
+    phases = read_all()
     # optional: the whole step captured once as a HIP graph and replayed (every kernel still
     # runs every step; the graph only removes host launch cost).  fia_prepare_for (large k)
     # decides the cache size on the host, so those configs run eagerly.
-    use_graph = args.graph and not big_k
+    use_graph = args.graph and not big_k and len(lanes) == 1
     graph = None
     if use_graph:
         side = torch.cuda.Stream(device=dev)
@@ -640,7 +693,8 @@ def main():
     per_step = {p: v[0] / n_instr for p, v in phases.items()}
     dom = max(("prepare", "solve", "score"), key=lambda p: per_step.get(p, 0.0))
     if not args.no_timed_events:
-        ctx.set_profiling(True, phases=tuple(sorted({"score", dom})))
+        for L in lanes:
+            L["ctx"].set_profiling(True, phases=tuple(sorted({"score", dom})))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -648,17 +702,18 @@ def main():
     for _ in range(args.steps):
         if graph is not None:
             graph.replay()
+            exchange()
         else:
-            compute()
-        exchange()
+            exchange(compute())
     if tg is not None:
         tg.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_profiling(False)
-    timed = ctx.profile_read()          # scoring kernel duration over the timed region
+    for L in lanes:
+        L["ctx"].set_profiling(False)
+    timed = read_all()          # scoring kernel duration over the timed region
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -698,6 +753,16 @@ def main():
                      args.traffic_json, ROOT)) if traffic else "no PMC traffic recorded for this config/kernel",
                  "algorithmic": {"model": "SURVEY.md 8d (gathered rows counted once per query)",
                                  "bytes_per_launch": alg_bytes, "gbs": alg_bytes / (score_ms * 1e-3) / 1e9}}
+    if len(lanes) > 1:
+        # batches in flight share the GPU, so the timed-region launch is longer than the
+        # kernel alone: the same bytes over the instrumented (one step at a time) launches too
+        iso = phases.get("score", (0.0, 0))
+        iso_ms = iso[0] / max(iso[1], 1)
+        score_hbm["isolated"] = {"kernel_ms": iso_ms,
+                                 "achieved": traffic / (iso_ms * 1e-3) / 1e9 if traffic and iso_ms > 0 else None,
+                                 "frac": traffic / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic and iso_ms > 0
+                                 else None,
+                                 "note": "instrumented steps run one at a time (no overlap with another batch)"}
     if dom == "score":
         roofline = dict(score_hbm, phase="score")
     else:
@@ -731,6 +796,13 @@ def main():
                     "traffic_gbs": dtraffic / (ph_ms * 1e-3) / 1e9 if dtraffic else None,
                     "traffic_scope": dtj.get("scope", "kernel " + dk + ", per dispatch") if dtj else None,
                     "score_hbm": score_hbm}
+        if len(lanes) > 1:
+            iso = phases.get(dom, (0.0, 0))
+            iso_ms = iso[0] / max(iso[1], 1)
+            roofline["isolated"] = {"kernel_ms": iso_ms,
+                                    "achieved": flops / (iso_ms * 1e-3) / 1e12 if iso_ms > 0 else None,
+                                    "frac": flops / (iso_ms * 1e-3) / 1e12 / FP64_PEAK_TFS if iso_ms > 0 else None,
+                                    "note": "instrumented steps run one at a time (no overlap with another batch)"}
     workload = cfg["workload"]
     if world > 1 and scaling == "weak":
         workload += " -- WEAK scaling: ranks > 0 answer synthetic re-paired queries of the same shape"
@@ -750,6 +822,7 @@ def main():
                    "query_order": args.query_order, "shard_of": shard_of,
                    "shard_index": (rank if world > 1 else args.shard_index) if shard_of > 1 else None,
                    "hip_graph": use_graph,
+                   "batches_in_flight": len(lanes),
                    "spinup_steps": n_spin,
                    "dist_backend": backend if world > 1 else None,
                    "parallelism": "dp%d (query shards, top-K all_gather)" % world},
@@ -764,7 +837,8 @@ def main():
         out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for L in lanes:
+        L["ctx"].close()
     if world > 1:
         dist.destroy_process_group()
 
