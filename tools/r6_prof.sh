@@ -5,7 +5,8 @@
 #   stats : the bench command itself under rocprofv3 --kernel-trace --stats; its JSON line is
 #           the committed bench line (HIP-event kernel times and the rocprof averages of one run)
 #           -> gpurun_out/r6prof/<name>/{stats,bench.json}
-# names: ml1m yelp m64 mf256 ncf256 ml1m8 (ml1m8: one shard of the 8-way split)
+# names: ml1m yelp m64 m64i2 mf256 ncf256 ml1m8 (ml1m8: one shard of the 8-way split; m64i2:
+# config 4 with two batches in flight)
 # Every step under its own time limit; the first failing step ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -15,6 +16,7 @@ declare -A ARGS=(
   [ml1m8]="--config ml1m-mf --shard-of 8 --shard-index 0"
   [yelp]="--config yelp-ncf"
   [m64]="--config 20m-mf64"
+  [m64i2]="--config 20m-mf64 --inflight 2"
   [mf256]="--config 20m-mf256 --shard-of 8"
   [ncf256]="--config 20m-ncf256 --shard-of 8"
 )

@@ -3,9 +3,10 @@ WRITE_SIZE, separate runs) -> profiles/traffic.json, {config: {kernel: entry}}.
 
     python tools/traffic_json.py <config> <fetch_dir> <write_dir> <out.json> <kernel>...
 
-A <kernel> argument NAME=k1+k2+... records a phase: the bytes of all dispatches of k1, k2, ...
-divided by the dispatch count of k1 (the phase's first kernel, launched once per phase), as
-entry NAME (e.g. prepare_phase=k_gram_mf_stream+k_gram_combine).
+A <kernel> argument NAME=k1+k2+...[/anchor] records a phase: the bytes of all dispatches of k1,
+k2, ... divided by the dispatch count of the anchor (default k1; a kernel launched once per
+phase), as entry NAME (e.g. prepare_phase=k_gram_mf_stream+k_gram_combine,
+solve_phase=k_bs_dupd+k_bs_dfac+k_bs_trail+k_bs_back/k_big_prologue).
 
 MI355X_MICROARCH.md: FETCH_SIZE (KB) reports half the bytes of a wide coalesced read
 on gfx950 -> doubled; WRITE_SIZE (KB) taken as is."""
@@ -27,9 +28,11 @@ def dispatch_values(d, counter, kernel):
 
 
 def per_dispatch(d, counter, kernel):
-    if "=" in kernel:                       # a phase: all its kernels per dispatch of the first
-        ks = kernel.split("=", 1)[1].split("+")
-        first = dispatch_values(d, counter, ks[0])
+    if "=" in kernel:                       # a phase: all its kernels per dispatch of the anchor
+        spec = kernel.split("=", 1)[1]
+        spec, anchor = spec.split("/", 1) if "/" in spec else (spec, None)
+        ks = spec.split("+")
+        first = dispatch_values(d, counter, anchor or ks[0])
         if not first:
             return None, 0
         return sum(sum(dispatch_values(d, counter, k)) for k in ks) / len(first), len(first)
@@ -65,8 +68,11 @@ def main():
                          "runs); FETCH_SIZE(KB) x2 (gfx950 correction, MI355X_MICROARCH.md) + WRITE_SIZE(KB), "
                          "x1024, per-dispatch average"}
         if "=" in kern:
-            res["kernels"] = kern.split("=", 1)[1].split("+")
-            res["scope"] = "phase %s: every dispatch of %s per dispatch of the first" % (name, " + ".join(res["kernels"]))
+            spec = kern.split("=", 1)[1]
+            spec, anchor = spec.split("/", 1) if "/" in spec else (spec, None)
+            res["kernels"] = spec.split("+")
+            res["scope"] = "phase %s: every dispatch of %s per dispatch of %s" % (
+                name, " + ".join(res["kernels"]), anchor or res["kernels"][0])
         entry[name] = res
         print(json.dumps(res))
     allres[cfg] = entry
