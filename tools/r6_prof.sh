@@ -42,5 +42,7 @@ for n in "$@"; do
     step "$o/stats" 600 rocprofv3 --kernel-trace --stats -d "$o/stats" -o run --output-format csv -- \
       python3 bench.py $a ${BENCH_EXTRA:-}
     grep '^{"metric"' "$o/stats.log" | tail -1 > "$o/bench.json"
+    # keep the summary (kernel stats), drop the per-dispatch trace (tens of MB)
+    find "$o/stats" -name '*kernel_trace.csv' -delete
   fi
 done
