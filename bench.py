@@ -11,14 +11,19 @@ resident in HBM.
 Multi-GPU (one process per GPU).  `--gpus N` without a launcher
 re-launches this script under torch.distributed.run with N ranks before anything
 touches the GPU; under torchrun (the driver) WORLD_SIZE/RANK/LOCAL_RANK are read
-from the environment.  Scaling (`--scaling`; every config defaults to strong):
+from the environment.  Scaling (`--scaling`; the sub-ms ml-1m-ex / yelp-ex steps default to
+weak -- every rank answers a full-size query set, per-GPU work fixed as N grows -- and the
+20M configs, whose test queries the north star shards across the GPUs, to strong):
   * strong: the config's fixed query set is split into N contiguous ranges balanced
     by n_q + query_cost (the related-set size plus a per-query fixed cost, CONFIGS;
     influence.sharding.shard_ranges); every rank answers its range.  On one GPU, `--shard-of S --shard-index r` answers range r
     of an S-way split (one rank's share of an S-GPU job);
-  * weak (opt-in): every rank answers one full-size query set -- rank 0 the
-    workload's own pairs, rank r > 0 the same users and item multiset re-paired by
-    a seeded permutation (distinct pairs, none a training row).
+  * weak: every rank answers one full-size query set -- rank 0 the workload's own
+    pairs, rank r > 0 the same users and item multiset re-paired by a seeded
+    permutation (distinct pairs, none a training row).  A 1/8 strong split of the
+    0.1 ms ml-1m-ex step leaves each rank its fixed costs (the Gram pass is
+    latency-bound: a shard's marked pass takes as long as the full one), so that
+    split cannot scale (profiles/round6_shards.md).
 The only exchange is the RCCL all_gather of the per-query top-K lists, overlapped
 with the next step.
 
@@ -63,9 +68,9 @@ FP64_PEAK_TFS = 78.6       # MI355X dense FP64 (vector and matrix; tools/mb_f64.
 # query over 6.0 ps per scored rating
 CONFIGS = {
     "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m",
-                    scaling="strong", query_cost=560, inflight=2),
+                    scaling="weak", query_cost=560, inflight=2),
     "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp",
-                     scaling="strong", query_cost=210, inflight=2),
+                     scaling="weak", query_cost=210, inflight=2),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
                      k=64, data="20m", scaling="strong", query_cost=10100),
     "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "

@@ -111,8 +111,8 @@ def test_two_ranks_on_one_gpu_equal_single_process(model, k):
 def test_bench_two_ranks(scaling, tmp_path):
     """bench.py --gpus 2 (self-launched under torch.distributed.run; both ranks on cuda:0, so
     gloo carries the top-K exchange): one JSON line with n_gpus 2 and the node's total.  The
-    default is strong scaling of the real ml-1m-ex test set; weak scaling is opt-in and labels
-    its synthetic re-paired queries in config.workload."""
+    ml-1m-ex default is weak scaling (rank 1's synthetic re-paired queries are labelled in
+    config.workload); strong scaling splits the real test set."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
            "--no-cpu-baseline"] + ([] if scaling == "default" else ["--scaling", scaling])
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
@@ -120,7 +120,7 @@ def test_bench_two_ranks(scaling, tmp_path):
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
-    want = "strong" if scaling == "default" else scaling
+    want = "weak" if scaling == "default" else scaling
     assert out["n_gpus"] == 2 and out["scaling"] == want and out["value"] > 0
     sizes = out["config"]["queries_per_rank"]
     if want == "weak":
