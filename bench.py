@@ -482,6 +482,8 @@ def main():
         sys.exit(rc)
     cfg = CONFIGS[args.config]
     scaling = cfg["scaling"] if args.scaling == "auto" else args.scaling
+    if args.shard_of > 1 and args.scaling == "auto":
+        scaling = "strong"      # one rank's share of an S-way split of the query set
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
