@@ -469,42 +469,58 @@ class GenericNeuralNet(object):
             return self.get_influence_batch([test_index], K=0, full=True, return_x=True, inverse_hvp=inverse_hvp)
         n = int(self._deg_u[u] + self._deg_i[i])
         D = self.ctx.num_params()
-        dev = self.ctx.torch_device
         b = getattr(self, "_one_bufs", None)
         if b is None or b["cap"] < max(n, 1) or b["D"] != D:
             cap = max(n, 1024, 2 * (b["cap"] if b else 0))
-            b = dict(cap=cap, D=D,
-                     q=torch.empty(2, dtype=torch.int32, device=dev),
-                     off=torch.empty(2, dtype=torch.int64, device=dev),
-                     rel=torch.empty(cap, dtype=torch.int32, device=dev),
-                     infl=torch.empty(cap, dtype=torch.float64, device=dev),
-                     x=torch.empty(D, dtype=torch.float64, device=dev),
-                     hq=torch.empty(2, dtype=torch.int32, pin_memory=True),
-                     hoff=torch.empty(2, dtype=torch.int64, pin_memory=True),
-                     hrel=torch.empty(cap, dtype=torch.int32, pin_memory=True),
-                     hinfl=torch.empty(cap, dtype=torch.float64, pin_memory=True),
-                     hx=torch.empty(D, dtype=torch.float64, pin_memory=True))
-            self._one_bufs = b
-        b["hq"].numpy()[:] = (u, i)
-        b["q"].copy_(b["hq"], non_blocking=True)
+            b = self._one_alloc(cap, D)
+        b["hin"].numpy()[:2] = (u, i)
+        b["din"][:8].copy_(b["hin_all"][:8], non_blocking=True)
         qu, qi = b["q"][0:1], b["q"][1:2]
         self.ctx.count_related(qu, qi, b["off"], want_total=False)
         if inverse_hvp is not None:
             xin = np.ascontiguousarray(np.asarray(inverse_hvp, np.float64).reshape(-1))
             if xin.size != D:
                 raise ValueError("inverse_hvp must hold %d values" % D)
-            b["hx"].numpy()[:] = xin
-            b["x"].copy_(b["hx"], non_blocking=True)
-            self.ctx.query_batch_x(qu, qi, b["off"], n, b["x"], b["rel"], b["infl"], 0, None, None, None)
+            b["hxin"].numpy()[:] = xin
+            b["din"][8:].copy_(b["hin_all"][8:], non_blocking=True)
+            self.ctx.query_batch_x(qu, qi, b["off"], n, b["xin"], b["rel"], b["infl"], 0, None, None, None)
         else:
             self.ctx.query_batch(qu, qi, b["off"], n, b["rel"], b["infl"], b["x"], 0, None, None, None)
-        b["hoff"].copy_(b["off"], non_blocking=True)
-        b["hrel"][:n].copy_(b["rel"][:n], non_blocking=True)
-        b["hinfl"][:n].copy_(b["infl"][:n], non_blocking=True)
-        b["hx"].copy_(b["x"], non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        return dict(offsets=b["hoff"].numpy().copy(), rel_idx=b["hrel"][:n].numpy().astype(np.int64),
-                    influence=b["hinfl"][:n].numpy().copy(), x=b["hx"].numpy().copy().reshape(1, D))
+        # every result in one copy (offsets, rows, influence and x share one device block)
+        b["hout"].copy_(b["dout"], non_blocking=True)
+        torch.cuda.current_stream(self.ctx.torch_device).synchronize()
+        hv = b["hviews"]
+        x = hv["x"] if inverse_hvp is None else xin
+        return dict(offsets=hv["off"].copy(), rel_idx=hv["rel"][:n].astype(np.int64),
+                    influence=hv["infl"][:n].copy(), x=np.array(x, np.float64).reshape(1, D))
+
+    def _one_alloc(self, cap, D):
+        """_one_query's persistent blocks: in = {u, i} (+ a given x), out = {offsets[2], x[D],
+        influence[cap], rows[cap]} -- one device block and one pinned host block each way."""
+        import torch
+        dev = self.ctx.torch_device
+        n_in = 8 + 8 * D                         # two int32 ids (8 B), then x_in
+        o_off, o_x = 0, 16
+        o_infl = o_x + 8 * D
+        o_rel = o_infl + 8 * cap
+        n_out = o_rel + 4 * cap
+        din = torch.empty(n_in, dtype=torch.uint8, device=dev)
+        hin = torch.empty(n_in, dtype=torch.uint8, pin_memory=True)
+        dout = torch.empty(n_out, dtype=torch.uint8, device=dev)
+        hout = torch.empty(n_out, dtype=torch.uint8, pin_memory=True)
+        hnp = hout.numpy()
+        b = dict(cap=cap, D=D, din=din, dout=dout,
+                 hin=hin[:8].view(torch.int32), hxin=hin[8:].view(torch.float64), hout=hout,
+                 q=din[:8].view(torch.int32), xin=din[8:].view(torch.float64),
+                 off=dout[o_off:o_off + 16].view(torch.int64), x=dout[o_x:o_x + 8 * D].view(torch.float64),
+                 infl=dout[o_infl:o_infl + 8 * cap].view(torch.float64),
+                 rel=dout[o_rel:o_rel + 4 * cap].view(torch.int32),
+                 hviews=dict(off=hnp[o_off:o_off + 16].view(np.int64), x=hnp[o_x:o_x + 8 * D].view(np.float64),
+                             infl=hnp[o_infl:o_infl + 8 * cap].view(np.float64),
+                             rel=hnp[o_rel:o_rel + 4 * cap].view(np.int32)))
+        b["hin_all"] = hin
+        self._one_bufs = b
+        return b
 
     def _split_theta(self, x):
         raise NotImplementedError
