@@ -269,6 +269,9 @@ struct fia_ctx {
   bool l1_pending = false;
   unsigned profiling = 0;   // bit p: record phase p (fia_set_profiling)
   fia::PhaseEvents events;
+  // the chunk-list scan's timing events when that phase is its one kernel (stamped by its
+  // dispatch, no marker packets: query_impl sets them around build_chunks)
+  hipEvent_t scan_ev[2] = {nullptr, nullptr};
 };
 
 namespace fia {

@@ -800,10 +800,12 @@ static hipError_t launch_query_scan(fia_ctx* c, int64_t Q, const int32_t* qu, co
   FIA_HIP_TRY(c->flag.reserve(64, s));
   const int64_t ntiles = (Q + 1 + kScanTile - 1) / kScanTile;
   unsigned int* ctr = reinterpret_cast<unsigned int*>(c->qscan.as<char>() + c->qscan.bytes - 16);
-  hipLaunchKernelGGL(k_query_scan<MODE>, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s, qu, qi, Q,
-                     c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I, out,
-                     c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word, qbase, runs,
-                     clen, lsh, slices);
+  // (MODE 1: the caller's phase events, if any, stamped by this dispatch)
+  hipExtLaunchKernelGGL(k_query_scan<MODE>, dim3((unsigned)ntiles), dim3(kScanThreads), 0, s,
+                        MODE == 1 ? c->scan_ev[0] : nullptr, MODE == 1 ? c->scan_ev[1] : nullptr, 0, qu, qi, Q,
+                        c->idx.side[0].ptr.as<int64_t>(), c->idx.side[1].ptr.as<int64_t>(), c->idx.U, c->idx.I, out,
+                        c->qscan.as<unsigned long long>(), ctr, c->flag.as<int32_t>(), offsets, cdesc, zero_word, qbase,
+                        runs, clen, lsh, slices);
   return hipGetLastError();
 }
 

@@ -2799,15 +2799,30 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // the queries whose test pair is a train row are listed in `coupled` {count, q...} by the
   // solve and finished full-D; the chunk scan zeroes the count
   FIA_HIP_TRY(c->coupled.reserve(sizeof(int32_t) * (size_t)(Q + 1), s));
-  phase_begin(c, 4, s);
+  // MF k <= 16: the chunk phase is the one scan kernel and the solve phase the side-system solve
+  // + the coupled solve, so their events are stamped by those kernels' dispatches (a marker
+  // packet per event idled the GPU ~5 us: RQ2's single query)
+  constexpr bool ext_phases = runs && !M::ncf && use_quad_solve<M>();
+  PhaseSpan cspan;
+  if (ext_phases) {
+    cspan = phase_span(c, 4);
+    c->scan_ev[0] = cspan.a;
+    c->scan_ev[1] = cspan.b;
+  } else {
+    phase_begin(c, 4, s);
+  }
   // MF k <= 16 item runs: one wave per equal-cost slice of the descriptor list (descriptor
   // costs vary ~10x: a static stride over descriptors left waves idle for half the kernel);
   // the slice count is known on the device only -- the grid is its bound (total cost <=
   // kRunUserCost per descriptor slot), the surplus waves exit at once
   constexpr int64_t lam = kRunLambda;
   const int64_t runs_grid = (kRunUserCost * (max_chunks + 1)) / lam + 2;
-  FIA_HIP_TRY(build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs, (int)lam,
-                           M::ncf ? kNcfRunChunk : kRunChunk));
+  {
+    const hipError_t eb = build_chunks(c, Q, qu, qi, offsets, max_chunks, grouped, s, c->coupled.as<int32_t>(), runs,
+                                       (int)lam, M::ncf ? kNcfRunChunk : kRunChunk);
+    c->scan_ev[0] = c->scan_ev[1] = nullptr;
+    FIA_HIP_TRY(eb);
+  }
   if (grouped) FIA_HIP_TRY(build_groups(c, Q, qu, qi, offsets, max_items, qblock, s, use_mfma ? kMfmaCPI : 1));
   // the query-side work that needs no Gram cache, ahead of the join with a pending prepare:
   // NCF k = 16 the per-query MLP prologue (after the layer-1 rows), k <= 16 the d1 table
@@ -2831,9 +2846,12 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
       A.d1tab = c->d1tab.as<double>();
     }
   }
-  phase_end(c, 4, s);
+  if (!ext_phases) phase_end(c, 4, s);
   FIA_HIP_TRY(join_prepare(c, s));     // the Gram caches (and NCF rows) of a pending fia_prepare
-  phase_begin(c, 1, s);
+  const bool ext_solve = ext_phases && Q > 0 && !x_in;
+  PhaseSpan sspan;
+  if (ext_solve) sspan = phase_span(c, 1);
+  else phase_begin(c, 1, s);
   if (x_in && Q > 0) {
     // a given inverse HVP: records straight from it, no solve (fia_query_batch_x)
     const int64_t g1 = Q < 8192 ? Q : 8192;
@@ -2844,8 +2862,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
   // non-coupled queries: thread-per-system (MF k <= 16) or column-parallel blocks
   if (Q > 0 && !x_in) {
     if constexpr (use_quad_solve<M>()) {
-      hipLaunchKernelGGL(k_solve_quad<M>, dim3((unsigned)((Q + 7) / 8)), dim3(64), 0, s, A, Q, c->rec.as<double>(),
-                         x_out, c->coupled.as<int32_t>());
+      hipExtLaunchKernelGGL(k_solve_quad<M>, dim3((unsigned)((Q + 7) / 8)), dim3(64), 0, s, sspan.a, (hipEvent_t) nullptr, 0, A, Q,
+                            c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
     } else if constexpr (use_tps<M>()) {
       hipLaunchKernelGGL(k_solve_tps<M>, dim3((unsigned)((2 * Q + 63) / 64)), dim3(64), 0, s, A, Q,
                          c->rec.as<double>(), x_out, c->coupled.as<int32_t>());
@@ -2872,8 +2890,8 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     // ml-1m-ex: the full-D solve's LDS and registers in every workgroup)
     const int64_t gc = M::K <= 16 ? 64 : 256;
     const int64_t g2 = Q < gc ? Q : gc;
-    hipLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, A, Q, c->rec.as<double>(), x_out,
-                       (const int32_t*)c->coupled.as<int32_t>());
+    hipExtLaunchKernelGGL(k_solve<M>, dim3((unsigned)g2), dim3(kSolveThreads), 0, s, (hipEvent_t) nullptr,
+                          sspan.b, 0, A, Q, c->rec.as<double>(), x_out, (const int32_t*)c->coupled.as<int32_t>());
   }
   if constexpr (mask_path<M>()) {
     if (Q > 0) {       // the records' MLP block -> y = W1_side^T x_mlp for k_score_ncf
@@ -2882,7 +2900,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
     }
   }
   FIA_HIP_TRY(hipGetLastError());
-  phase_end(c, 1, s);
+  if (!ext_solve) phase_end(c, 1, s);
   int64_t grid = (max_items + 3) / 4;            // 4 waves (work items) per block
   if (grid < 1) grid = 1;
   // grid cap (measured): NCF 1024 workgroups (yelp-ex score 0.314 -> 0.290 ms), MF 8192

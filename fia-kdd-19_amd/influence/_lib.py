@@ -120,6 +120,7 @@ class Context(object):
         arr = (ctypes.c_void_p * len(tables))(*[t.data_ptr() for t in tables])
         self._keep = list(tables)
         self.full_prepared = False
+        self._num_params = None
         rc = self.lib.fia_set_params(self.h, model, k, U, I, arr, len(tables), float(wd), float(damping))
         self._check(rc, "fia_set_params")
 
@@ -141,7 +142,9 @@ class Context(object):
         self._check(self.lib.fia_prepare_for(self.h, qu.numel(), _ptr(qu), _ptr(qi), _stream()), "fia_prepare_for")
 
     def num_params(self):
-        return self.lib.fia_num_params(self.h)
+        if getattr(self, "_num_params", None) is None:
+            self._num_params = self.lib.fia_num_params(self.h)
+        return self._num_params
 
     # ---- queries ----
     def count_related(self, qu, qi, offsets=None, want_total=True):
@@ -204,11 +207,14 @@ class Context(object):
     def _set_mask(self, mask):
         self._check(self.lib.fia_set_profiling(self.h, mask), "fia_set_profiling")
         self._mask = mask
+        if mask:
+            self._pending = True    # events may be recorded until the next drain
 
     def _drain(self):
         ms = (ctypes.c_double * FIA_NUM_PHASES)()
         cnt = (ctypes.c_int64 * FIA_NUM_PHASES)()
         self._check(self.lib.fia_profile_read(self.h, ms, cnt), "fia_profile_read")
+        self._pending = self._mask != 0
         return {PHASES[p]: (ms[p], cnt[p]) for p in range(FIA_NUM_PHASES)}
 
     def profile_read(self):
@@ -223,7 +229,8 @@ class Context(object):
         """Run fn() with every phase recorded and return (fn's result, its phase sums).  The
         caller's profiling mask and the sums it has accumulated but not yet read are kept
         (the RQ2 timers of a single query, GenericNeuralNet.get_influence_on_test_loss)."""
-        before = self._drain()
+        # (nothing can be pending when profiling was off since the last drain: skip that read)
+        before = self._drain() if getattr(self, "_pending", True) else {p: (0.0, 0) for p in PHASES}
         mask = self._mask
         self._set_mask(0x1f)
         try:

@@ -29,8 +29,10 @@ def main():
     m = RQ2.build("movielens", "MF", cfg, ds, train_dir="/tmp/rq2b")
     t = 59
     N = ds["train"].labels.shape[0]
-    m.get_influence_on_test_loss([t], np.arange(N))
-    print("facade call (RQ2 timers)  %.1f us" % med(lambda: m.get_influence_on_test_loss([t], np.arange(N))))
+    ar = np.arange(N)
+    m.get_influence_on_test_loss([t], ar)
+    print("facade call (RQ2 timers)   %.1f us" % med(lambda: m.get_influence_on_test_loss([t], ar)))
+    print("  its own wall (last_timing) %.1f us" % (m.last_timing["wall_s"] * 1e6))
     print("one-sync path, no timers   %.1f us" % med(lambda: m._one_query(t)))
     b = m._one_bufs
     u, i = m._test_pair(t)
