@@ -1011,6 +1011,15 @@ __host__ __device__ constexpr int64_t bs_slab() {   // L, d, W, then L11^-1 of e
   return (int64_t)(NP + 16) * NP + NP + kBsNB * kBsNB + (int64_t)((NP + kBsNB - 1) / kBsNB) * kBsNB * kBsNB;
 }
 
+// Panel layout: when NP is not a multiple of 64 the NARROW panel comes first (columns
+// [0, NP % 64)), then 64-column panels -- the narrow panel then has no update k-steps (no
+// factored columns left of it), where as the last panel its k_bs_dupd / k_bs_trail were
+// long single-wave chains over every earlier column for 16 columns of work (MF k = 256:
+// 1.7 of 14 ms per batch).  Panel starting at column c0 keeps its L11^-1 in slot
+// ceil(c0 / 64), so the first panel is slot 0 in both layouts.
+__host__ __device__ constexpr int bs_first_panel(int NP) { return NP % kBsNB == 0 ? kBsNB : NP % kBsNB; }
+__host__ __device__ constexpr int bs_panel_slot(int c0) { return (c0 + kBsNB - 1) / kBsNB; }
+
 // wave-local LDS hand-off: a wave's LDS operations complete in order; this only keeps
 // the compiler from moving them across the exchange
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1149,39 +1158,50 @@ __global__ __launch_bounds__(64) void k_bs_dfac(const int32_t* __restrict__ list
   double* __restrict__ dd = Ls + (int64_t)LDR * NP;
   double* __restrict__ W = dd + NP;
   const int lane = threadIdx.x;
-  // entries right of a lane's diagonal become garbage and are never read
-  double a[NB];
+  // only the NBE x NBE block is factored (a narrow panel: the chains are NBE long); the
+  // inverse is identity-padded to 64 x 64 below.  Entries right of a lane's diagonal
+  // become garbage and are never read
+  double a[NBE];
 #pragma unroll
-  for (int t = 0; t < NB; ++t) a[t] = W[t * NB + lane];      // block stored column-major
+  for (int t = 0; t < NBE; ++t) a[t] = W[t * NB + lane];     // block stored column-major
 #pragma unroll
-  for (int j = 0; j < NB; ++j) {
+  for (int j = 0; j < NBE; ++j) {
     const double dj = readlane_dbl(a[j], j);
     const double f = lane > j ? a[j] / dj : 0.0;
 #pragma unroll
-    for (int t = j + 1; t < NB; ++t) a[t] = fma(-f, readlane_dbl(a[j], t), a[t]);
+    for (int t = j + 1; t < NBE; ++t) a[t] = fma(-f, readlane_dbl(a[j], t), a[t]);
   }
   double dl = a[0];
 #pragma unroll
-  for (int t = 1; t < NB; ++t) dl = t == lane ? a[t] : dl;
+  for (int t = 1; t < NBE; ++t) dl = t == lane ? a[t] : dl;
   if (lane < NBE) dd[c0 + lane] = dl;
   const double rdl = 1.0 / dl;
 #pragma unroll
-  for (int t = 0; t < NB; ++t) {                            // a[t] becomes L11[lane][t], t < lane
+  for (int t = 0; t < NBE; ++t) {                           // a[t] becomes L11[lane][t], t < lane
     a[t] = t < lane ? a[t] * readlane_dbl(rdl, t) : 0.0;
     if (t < lane && lane < NBE) Ls[(int64_t)(c0 + t) * LDR + c0 + lane] = a[t];
   }
-  // lane j: column j of L11^-1 (x_m = 0 for m < j)
-  double x[NB];
+  // lane j: column j of L11^-1 (x_m = 0 for m < j); lanes j >= NBE: identity columns
+  double x[NBE];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) {
+  for (int i = 0; i < NBE; ++i) {
     double s = i == lane ? 1.0 : 0.0;
 #pragma unroll
     for (int m = 0; m < i; ++m) s = fma(-readlane_dbl(a[m], i), x[m], s);
     x[i] = s;
   }
-  double* __restrict__ Xp = W + NB * NB + (int64_t)(c0 / NB) * NB * NB;
+  double* __restrict__ Xp = W + NB * NB + (int64_t)bs_panel_slot(c0) * NB * NB;
 #pragma unroll
-  for (int n = 0; n < NB; ++n) Xp[n * NB + (lane ^ (4 * (n & 7)))] = x[n];
+  for (int n = 0; n < NB; ++n) {
+    double xn = n == lane ? 1.0 : 0.0;
+    if constexpr (NBE < NB) {
+#pragma unroll
+      for (int i = 0; i < NBE; ++i) xn = n == i ? x[i] : xn;
+    } else {
+      xn = x[n < NBE ? n : 0];
+    }
+    Xp[n * NB + (lane ^ (4 * (n & 7)))] = xn;
+  }
 }
 
 template <class M, int NP, int NBE>
@@ -1203,7 +1223,7 @@ __global__ __launch_bounds__(256) void k_bs_trail(BigArgs A, const int32_t* __re
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ml = lane & 15, kl = lane >> 4;
   double* __restrict__ Ls = lscr + (int64_t)sys * bs_slab<NP>();
   const double* __restrict__ dd = Ls + (int64_t)LDR * NP;
-  const double* __restrict__ W = dd + NP + NB * NB + (int64_t)(c0 / NB) * NB * NB;   // this panel's L11^-1
+  const double* __restrict__ W = dd + NP + NB * NB + (int64_t)bs_panel_slot(c0) * NB * NB;   // this panel's L11^-1
   // L11^-1 of this panel (k_bs_dfac) into LDS by DMA, landing while the panel update runs
 #pragma unroll
   for (int i = 0; i < NB * NB / 512; ++i)
@@ -1315,17 +1335,20 @@ __global__ __launch_bounds__(512) void k_bs_back(BigArgs A, const int32_t* __res
   const double* __restrict__ Ls = lscr + (int64_t)blockIdx.x * bs_slab<NP>();
   const double* __restrict__ X = Ls + (int64_t)LDR * NP + NP + NB * NB;
   const int tid = threadIdx.x;
-  // L^T x = y, y_c = L[NP][c].  Per 64-column block b from the end: x_b = L_bb^-T z_b with
-  // the panel's stored inverse (z_b: y_b after the later blocks' updates), then
-  // z_c -= sum_t L[b0 + t][c] x_b[t] for every earlier c.  One global round trip per block.
+  // L^T x = y, y_c = L[NP][c].  Per panel b from the end (64 columns; a narrow first
+  // panel, bs_first_panel): x_b = L_bb^-T z_b with the panel's stored inverse (z_b: y_b after
+  // the later blocks' updates), then z_c -= sum_t L[b0 + t][c] x_b[t] for every earlier c.
+  // One global round trip per block.
   for (int c = tid; c < NP + NB; c += kST) xs[c] = c < NP ? Ls[(int64_t)c * LDR + NP] : 0.0;
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  for (int b0 = ((NP - 1) / NB) * NB; b0 >= 0; b0 -= NB) {
-    const int bw = NP - b0 < NB ? NP - b0 : NB;
+  for (int b0 = NP - NB, bend = NP; bend > 0; bend = b0, b0 -= NB) {
+    const int bw = b0 < 0 ? bend : NB;
+    b0 = b0 < 0 ? 0 : b0;
     if (tid < bw) {
       // (L^-T)[c][n] = (L^-1)[n][c], zero for n < c and (identity padding) for n >= bw
-      const double* __restrict__ Xb = X + (int64_t)(b0 / NB) * NB * NB;
+      // (the padding's off-diagonal blocks are zero, so z entries past the block drop out)
+      const double* __restrict__ Xb = X + (int64_t)bs_panel_slot(b0) * NB * NB;
       double xc = 0.0;
 #pragma unroll 8
       for (int n = 0; n < NB; ++n) xc = fma(Xb[n * NB + (tid ^ (4 * (n & 7)))], xs[b0 + n], xc);
@@ -1909,7 +1932,7 @@ hipError_t launch_bs_panel(fia_ctx* c, const BigArgs& A, int64_t w0, int64_t n, 
 template <class M, int NP>
 hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, const int32_t* list, hipStream_t s) {
   static_assert(NP % 16 == 0, "side blocks are whole 16-column tiles");
-  constexpr int kLast = NP % kBsNB == 0 ? kBsNB : NP % kBsNB;   // last panel's width
+  constexpr int kFirst = bs_first_panel(NP);   // first panel's width
   if (max_sys <= 0) return hipSuccess;
   constexpr int64_t slab = bs_slab<NP>();
   int64_t S = kBsScratch / (int64_t)(sizeof(double) * slab);
@@ -1917,12 +1940,9 @@ hipError_t launch_solve_batched(fia_ctx* c, const BigArgs& A, int64_t max_sys, c
   FIA_HIP_TRY(c->lscr.reserve(sizeof(double) * (size_t)(S * slab), s));
   for (int64_t w0 = 0; w0 < max_sys; w0 += S) {
     const int64_t n = max_sys - w0 < S ? max_sys - w0 : S;
-    for (int c0 = 0; c0 < NP; c0 += kBsNB) {
-      if (NP - c0 >= kBsNB)
-        FIA_HIP_TRY((launch_bs_panel<M, NP, kBsNB>(c, A, w0, n, c0, list, s)));
-      else
-        FIA_HIP_TRY((launch_bs_panel<M, NP, kLast>(c, A, w0, n, c0, list, s)));
-    }
+    // the narrow panel (if any) first, then 64-column panels (bs_first_panel)
+    FIA_HIP_TRY((launch_bs_panel<M, NP, kFirst>(c, A, w0, n, 0, list, s)));
+    for (int c0 = kFirst; c0 < NP; c0 += kBsNB) FIA_HIP_TRY((launch_bs_panel<M, NP, kBsNB>(c, A, w0, n, c0, list, s)));
     hipLaunchKernelGGL((k_bs_back<M, NP>), dim3((unsigned)n), dim3(512), 0, s, A, list, (int)w0,
                        c->qwork.as<double>(), c->lscr.as<double>(), c->xb.as<double>(), c->rec.as<double>());
     FIA_HIP_TRY(hipGetLastError());
