@@ -183,14 +183,18 @@ def solve_kernel(cfg):
 
 def prepare_kernel(cfg):
     """The library's Gram pass for this config (models.hip prepare_impl, bigk.hip prepare_big).
-    MF k <= 16 is two kernels: the Gram stream and the combine of sliced lists' partial Grams
-    (traffic.json holds their sum per step as the "prepare_phase" entry)."""
+    MF k <= 16 is two kernels: the Gram stream and the combine of sliced lists' partial Grams;
+    MF k in {32, 64} the Gram kernel and the per-side residual pass (traffic.json holds each sum
+    per step as the "prepare_phase" entry)."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_big_gram"
     if model == "NCF":
         return "k_ncf_gram_rows"
-    return "k_gram_mf_stream + k_gram_combine" if k <= 16 else "k_gram_mf_mfma"
+    if k <= 16:
+        return "k_gram_mf_stream + k_gram_combine"
+    # k in {32, 64}: + the list-ordered residuals k_score_mf_mfma reads (k_lres_mf, both sides)
+    return "k_gram_mf_mfma + k_lres_mf"
 
 
 def side_dim(model, k):
@@ -415,12 +419,14 @@ def load_traffic(path, config, kernel):
 def compulsory_bytes(cfg, qu, qi, deg_u, deg_i, bounds):
     """Bytes the scoring kernel cannot avoid, per launch (mean over the batches): its outputs
     (8 B influence + 4 B train row per related rating) and every list entry of the batch's
-    users and items read once (4 B row + 4 B other id + 4 B rating)."""
+    users and items read once (4 B row + 4 B other id + 4 B rating; MF k in {32, 64}: the 8 B
+    list-ordered residual k_score_mf_mfma reads instead of the rating)."""
+    ent = 16.0 if cfg["model"] == "MF" and cfg["k"] in (32, 64) else 12.0
     tot = 0.0
     for b0, b1 in zip(bounds[:-1], bounds[1:]):
         u, i = qu[b0:b1], qi[b0:b1]
         out = 12.0 * float(deg_u[u].sum() + deg_i[i].sum())
-        lists = 12.0 * float(deg_u[np.unique(u)].sum() + deg_i[np.unique(i)].sum())
+        lists = ent * float(deg_u[np.unique(u)].sum() + deg_i[np.unique(i)].sum())
         tot += out + lists
     return tot / max(len(bounds) - 1, 1)
 

@@ -47,7 +47,7 @@ constexpr int kGsRing = 8;              // gathered sub-batches in the kernel's 
 constexpr int kGsMaxSub = 48;           // most sub-batches of one wave's range (a multiple of kGsRing)
 constexpr int kGsMaxSeg = 4;            // most segments (Grams) of one wave's range: staged in LDS,
                                         // stored when the range is done
-constexpr int kMfmaQB = 15;             // queries per MF k in {32, 64} MFMA scoring work item (+ the entity)
+constexpr int kMfmaQB = 16;             // queries per MF k in {32, 64} MFMA scoring work item
 constexpr int kMfmaCPI = 4;             // list chunks per MFMA scoring work item
 constexpr int kWgBlocks = 4;            // query blocks (one per wave) sharing a workgroup's gathered rows
 constexpr int kQueryBlock = 8;           // queries per entity-shared scoring work item (small k; 16 measured no better)

@@ -1647,15 +1647,24 @@ struct GramSides {
   const uint8_t* mark;
   int64_t moff[2];
   __device__ bool skip(int sd, int32_t e) const { return mark && !mark[moff[sd] + e]; }
+  // MF k in {32, 64} (k_gram_mf_mfma): the residual e_p = r-hat_p - y_p of every list
+  // position of a cached entity into lres[sd * N + p] for k_score_mf_mfma (nullptr: none)
+  const float* emb_self[2];
+  const float* rating[2];
+  const float* bias[2];       // user, item bias tables
+  const float* gb;
+  double* lres;
 };
 
 
 template <class M>
-__global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_gram_mf_mfma(GramSides GSd) {
   constexpr int K = M::K, Ds = M::Ds, GS = Ds * (Ds + 1) / 2, GSP = (GS + 1) & ~1;
   constexpr int NT = (K + 15) / 16;               // 16-wide column tiles
   constexpr int NP = NT * (NT + 1) / 2;           // upper tile pairs
-  constexpr int SUB = NT <= 2 ? 16 : 8;           // MFMA row-quads gathered ahead per batch
+  // MFMA row-quads gathered ahead per batch (k = 64: 6, so the double-buffered rows, the
+  // residual pass and the 10 accumulator tiles fit two waves per SIMD)
+  constexpr int SUB = NT <= 2 ? 16 : NT == 3 ? 8 : 6;
   const int sd = (int64_t)blockIdx.x >= GSd.n_items[0] ? 1 : 0;
   const int64_t w = (int64_t)blockIdx.x - (sd ? GSd.n_items[0] : 0);
   if (w >= GSd.n_items[sd]) return;
@@ -1704,18 +1713,60 @@ __global__ __launch_bounds__(64) void k_gram_mf_mfma(GramSides GSd) {
     }
   };
   if constexpr (K >= 32) {
+    // the residual of each gathered row (mf:89-116): the entity's own row dotted with it --
+    // lane (grp, col) holds coordinates 16 t + col of row 4 sb + grp, so a row's dot is a
+    // 16-lane DPP sum; lane l < 4 SUB then owns batch row l (its list entry, rating and the
+    // other side's bias, loaded with the row's gather one batch ahead).  The products and the
+    // sum order are the same from either side's list, so both copies have the same bits.
+    const bool want_res = GSd.lres != nullptr;
+    const float* __restrict__ es = GSd.emb_self[sd] + (int64_t)e * K;
+    double eself[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) eself[t] = 16 * t + col < K ? (double)es[16 * t + col] : 0.0;
+    const double bself = want_res ? (double)GSd.bias[sd][e] : 0.0, gbias = want_res ? (double)GSd.gb[0] : 0.0;
+    const float* __restrict__ bother = GSd.bias[1 - sd];
+    const int64_t lp0 = ptr[e] + start;
+    const float* __restrict__ ratp = GSd.rating[sd] + lp0;
+    auto row_loads = [&](int32_t id, int t0, float& y, float& bo) {
+      const bool ok = want_res && lane < 4 * SUB && t0 + lane < len;
+      y = ok ? ratp[t0 + lane] : 0.0f;
+      bo = ok && id >= 0 ? bother[id] : 0.0f;
+    };
+    auto residuals = [&](const double (&val)[SUB][NT], float y, float bo, int t0) {
+      double r = 0.0;
+#pragma unroll
+      for (int sb = 0; sb < SUB; ++sb) {
+        double part = 0.0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) part = fma(eself[t], val[sb][t], part);
+        const double v = __shfl(row_sum16(part), 16 * (lane & 3));
+        r = (lane >> 2) == sb ? v : r;
+      }
+      if (lane < 4 * SUB && t0 + lane < len) {
+        const double bu = sd == 0 ? bself : (double)bo, bi = sd == 0 ? (double)bo : bself;
+        GSd.lres[sd * GSd.N + lp0 + t0 + lane] = ((r + bu) + bi) + gbias - (double)y;
+      }
+    };
     double val[SUB][NT];
-    gather(ids_at(0), val);
+    int32_t id_c = ids_at(0);
+    gather(id_c, val);
+    float y_c, bo_c;
+    row_loads(id_c, 0, y_c, bo_c);
     int32_t id_n = ids_at(4 * SUB);
     for (int t0 = 0; t0 < len; t0 += 4 * SUB) {
       const int32_t id_nn = ids_at(t0 + 8 * SUB);
       double vn[SUB][NT];
       gather(id_n, vn);                          // next batch (ids -1 past the end)
+      float y_n, bo_n;
+      row_loads(id_n, t0 + 4 * SUB, y_n, bo_n);
+      if (want_res) residuals(val, y_c, bo_c, t0);
       accumulate(val);
 #pragma unroll
       for (int sb = 0; sb < SUB; ++sb)
 #pragma unroll
         for (int t = 0; t < NT; ++t) val[sb][t] = vn[sb][t];
+      y_c = y_n;
+      bo_c = bo_n;
       id_n = id_nn;
     }
   } else {
@@ -2755,6 +2806,18 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
     }
     return hipSuccess;
   } else {
+    if constexpr (K == 32 || K == 64) {
+      // list-ordered residuals of both sides for k_score_mf_mfma ([0, N) users, [N, 2N) items),
+      // written by the Gram pass for every list position of a cached entity
+      FIA_HIP_TRY(c->resid.reserve(sizeof(double) * (size_t)(2 * X.N + 1), s));
+      for (int sd = 0; sd < 2; ++sd) {
+        G.emb_self[sd] = c->p.t[sd];
+        G.rating[sd] = X.side[sd].rating.as<float>();
+        G.bias[sd] = c->p.t[2 + sd];
+      }
+      G.gb = c->p.t[4];
+      G.lres = c->resid.as<double>();
+    }
     if (G.n_items[0] + G.n_items[1] > 0) {
       hipLaunchKernelGGL(k_gram_mf_mfma<M>, dim3((unsigned)(G.n_items[0] + G.n_items[1])), dim3(64), 0, s, G);
       FIA_HIP_TRY(hipGetLastError());
@@ -2777,7 +2840,7 @@ hipError_t query_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* q
                       const double* x_in) {
   // One scoring schedule per (model, k, K) (measured on MI355X, profiles/): k <= 16 item runs
   // (MF k_score_mf_runs, NCF k_score_ncf_runs: per-query chunks sharing the item's list); MF
-  // k in {32, 64} entity-shared, on f64 MFMA for K <= 1 (k_score_mf_mfma, query blocks of 15)
+  // k in {32, 64} entity-shared, on f64 MFMA for K <= 1 (k_score_mf_mfma, query blocks of 16)
   // and on VALU otherwise (k_score_grouped_mf); NCF k = 32 entity-shared (k_score_ncf)
   constexpr bool grouped = M::ncf ? !mask_path<M>() : M::K >= 32;
   constexpr bool mfma_ok = !M::ncf && (M::K == 32 || M::K == 64);

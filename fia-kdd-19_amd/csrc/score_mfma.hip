@@ -2,13 +2,14 @@
 // kernel).  Reference: influence_j = x . grad L(z_j) / n for every related rating j of a test
 // rating (u, i) (src/influence/matrix_factorization.py:237-246), x = H_t^-1 v from the solve.
 //
-// A work item is <= kMfmaCPI chunks of 256 ratings of one entity's list x <= 15 batch queries
+// A work item is <= kMfmaCPI chunks of 256 ratings of one entity's list x <= 16 batch queries
 // sharing the entity (build_groups).  Per 16-rating tile the scores of every (query, rating)
 // pair are one 16x16 tile
 //   D = X . G^T      (v_mfma_f64_16x16x4_f64, K/4 slices of 4 coordinates)
-// with A rows = the block's queries' x (side block, k coordinates) and row 15 = the entity's
-// own embedding, so D[15][n] = theta_e . g_n gives the rating's residual e_n = r-hat_n - y_n
-// without a VALU dot product.  Slice s pairs coordinate (K/4) kk + s of lane group
+// with A rows = the block's 16 queries' x (side block, k coordinates).  The rating's residual
+// e_n = r-hat_n - y_n comes from the prepare's list-ordered residuals (k_lres_mf, read with the
+// list entries; round 6: row 15 of A was the entity's embedding, D[15][n] the residual's dot --
+// 1/16 of the MFMAs and the other side's bias gather per tile).  Slice s pairs coordinate (K/4) kk + s of lane group
 // kk = l >> 4: every lane loads K/4 CONTIGUOUS coordinates of its query's x (once per work
 // item) and of its rating's gathered row (per tile, 16-B loads).  MI355X runs f64 MFMA and f64
 // VALU on the same units (tools/mb_f64.hip: their times add), so the epilogue keeps f64 work
@@ -23,15 +24,15 @@
 // were a wave's largest cost: rows from row 0 instead of the real ones ran 2.39 vs 3.10 ms per
 // config-4 batch, no stores 3.33, no MFMAs 2.73 (same-box ablations) -- the random rows come
 // from the Infinity Cache, and the CU's outstanding misses, not bandwidth, bound them.  A
-// work item is now (entity chunks) x (a group of kWgBlocks = 4 query blocks of 15): the
+// work item is now (entity chunks) x (a group of kWgBlocks = 4 query blocks of 16): the
 // workgroup's four waves score the same tiles, one query block each, and the rows of a tile
 // are gathered ONCE per workgroup -- wave h fetches rows 4h .. 4h+3 (one 16-B piece per lane,
 // three tiles ahead, into a 3-slot register ring), writes them to a 3-slot LDS ring one tile
 // ahead, and one barrier per tile publishes them; each wave reads its B operand from LDS.
 // Rows in LDS are XOR-swizzled by 16-B piece (piece u of row r holds source piece u ^ r), so
 // the 16 rows of a B-operand read hit 16 different bank groups.  Entity groups with more than
-// 15 queries (95 % of the config-4 tiles are item-side, 14.8 live rows of 15 per tile) share
-// every gathered row among up to 60 queries: 3.3x fewer row gathers per batch
+// 16 queries (95 % of the config-4 tiles are item-side, almost all rows live) share
+// every gathered row among up to 64 queries: 3.3x fewer row gathers per batch
 // (tools/m64_occupancy.py).  The list entries come in blocks of 64 (one per lane, a block
 // issued eight tiles before its first tile), broadcast per tile by permlane swaps.
 #include <type_traits>
@@ -59,9 +60,10 @@ __device__ __forceinline__ unsigned bcast_row(unsigned x) {
   const auto l16 = __builtin_amdgcn_permlane16_swap(y, y, false, false);
   return (R & 1) ? l16[1] : l16[0];
 }
-__device__ __forceinline__ double bcast_row3_d(double x) {
+template <int R>
+__device__ __forceinline__ double bcast_row_d(double x) {
   const long long b = __double_as_longlong(x);
-  const unsigned lo = bcast_row<3>((unsigned)(b & 0xffffffffll)), hi = bcast_row<3>((unsigned)(b >> 32));
+  const unsigned lo = bcast_row<R>((unsigned)(b & 0xffffffffll)), hi = bcast_row<R>((unsigned)(b >> 32));
   return __longlong_as_double(((long long)hi << 32) | lo);
 }
 
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
   static_assert(LSL >= 16 * K, "a tile fits its slot");
   __shared__ __attribute__((aligned(16))) float lr0[LSL], lr1[LSL], lr2[LSL];
   __shared__ int32_t ccs[kWgBlocks][16][2];     // per query row: candidate slot base, position base
-  // each wave's A operand (its 15 queries' x + the entity row), rows padded by two doubles so
+  // each wave's A operand (its 16 queries' x), rows padded by two doubles so
   // the 16 rows of a read fall on 16 bank groups
   constexpr int AST = K + 2;
   __shared__ __attribute__((aligned(16))) double sA[kWgBlocks][16 * AST];
@@ -120,7 +122,6 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kk = lane >> 4, cn = lane & 15;     // k-group; A row / B column / D column
   const int64_t n_items = wstart[nE];
-  const double gbias = (double)A.t[4][0];
   // this lane's staged piece: row fr of the tile, LDS piece lane % SG holds source piece fs
   const int fr = RPW * wave + lane / SG, fs = (lane % SG) ^ (fr % SG);
   for (int64_t wi = blockIdx.x; wi < n_items; wi += gridDim.x) {
@@ -140,16 +141,14 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
     const float* __restrict__ rat = A.rating[sd] + lb;
     const int32_t* __restrict__ rwp = A.row[sd] + lb;
     const float* __restrict__ T = sd == 0 ? A.t[1] : A.t[0];     // the other side's table
-    const float* __restrict__ bt = sd == 0 ? A.t[3] : A.t[2];
-    const float* __restrict__ Es = sd == 0 ? A.t[0] : A.t[1];    // this side's (the entity's) table
-    const double bself = (double)(sd == 0 ? A.t[2] : A.t[3])[e];
+    const double* __restrict__ res = A.lres + (int64_t)sd * A.N + lb;   // e_j by list position
     // list blocks: entry 64 b + lane of the item (clamped to its last entry past the end)
     int32_t lo[kBlkRing], lw[kBlkRing];
-    float ly[kBlkRing];
+    double le[kBlkRing];
     auto load_block = [&](int b, int slot) {
       const int p = kBlk * b + lane < len ? kBlk * b + lane : len - 1;
       lo[slot] = oth[p];
-      ly[slot] = rat[p];
+      le[slot] = res[p];
       lw[slot] = rwp[p];
     };
     load_block(0, 0);
@@ -162,14 +161,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
     // fewer chunks, fia_query_batch; registers are what bounds this kernel's occupancy)
     bool qv[4] = {false, false, false, false};
     if (nq > 0) {
-      if (cn == 15) {
-        const float4* src = reinterpret_cast<const float4*>(Es + (int64_t)e * K + KS * kk);
-#pragma unroll
-        for (int f = 0; f < NF4; ++f) {
-          const float4 t = src[f];
-          a[4 * f] = t.x; a[4 * f + 1] = t.y; a[4 * f + 2] = t.z; a[4 * f + 3] = t.w;
-        }
-      } else {
+      {
         const int32_t q = gq[gb + (cn < nq ? cn : nq - 1)];
         const double2* src =
             reinterpret_cast<const double2*>(rec + (int64_t)q * M::R + 4 + sd * M::SB + K + KS * kk);
@@ -224,18 +216,14 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
     double prv[4] = {0.0, 0.0, 0.0, 0.0};     // previous tile's rotated values (aligned stores)
     int32_t prw[4] = {0, 0, 0, 0};
     const int ntl = (len + 15) / 16;
-    // staging: this lane's piece of the rows of tiles t+1 .. t+3 (fetching waves), and the
-    // other side's bias of this lane's column for the same tiles (every wave)
+    // staging: this lane's piece of the rows of tiles t+1 .. t+3 (fetching waves)
     f4v stg[kRing];
-    float sbo[4];          // (by tile % 4: fetched three tiles before its tile reads it)
     // tile at compile-time position J of the 12-tile period: its block slot and row of 16
     auto fetch = [&](auto jc, auto sc) {
       constexpr int J = decltype(jc)::value, slot = decltype(sc)::value;
       constexpr int BS = (J / kBlkTiles) % kBlkRing, BR = J % kBlkTiles;
       const int32_t of = __shfl((int)lo[BS], (BR * 16 + fr) & 63);
       stg[slot] = *reinterpret_cast<const f4v*>(T + (int64_t)of * K + 4 * fs);
-      const int32_t ob = (int32_t)bcast_row<BR>((unsigned)lo[BS]);
-      sbo[J % 4] = bt[ob];
     };
     auto stage = [&](auto sc) {
       constexpr int slot = decltype(sc)::value;
@@ -301,10 +289,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
       constexpr int BS = (J / kBlkTiles) % kBlkRing, BR = J % kBlkTiles;
       const int32_t o = (int32_t)bcast_row<BR>((unsigned)lo[BS]);
       const int32_t w = (int32_t)bcast_row<BR>((unsigned)lw[BS]);
-      const double y = (double)__uint_as_float(bcast_row<BR>(__float_as_uint(ly[BS])));
-      // residual of rating cn: D[15][cn] lives in lane 48 + cn, register 3
-      const double dself = bcast_row3_d(acc[3]);
-      const double en = ((dself + bself) + (double)sbo[J % 4]) + gbias - y;
+      const double en = bcast_row_d<BR>(le[BS]);                 // e of rating cn
       double al[4], be[4], xb[4];
       int32_t dupo[4], dl[4];
       uint32_t oofs[4];
@@ -332,6 +317,7 @@ __global__ __launch_bounds__(kScoreThreads) __attribute__((amdgpu_waves_per_eu(3
           if (!(pv && qv[r] && o == dupo[r])) continue;
           const int32_t q = gq[gb + kk + 4 * r];
           const double* __restrict__ R = rec + (int64_t)q * M::R;
+          const double y = (double)rat[p];
           val[r] = fma((R[3] - y) * al[r], R[2], be[r]);
         }
       }
