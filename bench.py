@@ -183,18 +183,15 @@ def solve_kernel(cfg):
 
 def prepare_kernel(cfg):
     """The library's Gram pass for this config (models.hip prepare_impl, bigk.hip prepare_big).
-    MF k <= 16 is two kernels: the Gram stream and the combine of sliced lists' partial Grams;
-    MF k in {32, 64} the Gram kernel and the per-side residual pass (traffic.json holds each sum
-    per step as the "prepare_phase" entry)."""
+    MF k <= 16 is two kernels: the Gram stream and the combine of sliced lists' partial Grams
+    (traffic.json holds their sum per step as the "prepare_phase" entry)."""
     k, model = cfg["k"], cfg["model"]
     if k >= 128 or (model == "NCF" and k >= 64):
         return "k_big_gram"
     if model == "NCF":
         return "k_ncf_gram_rows"
-    if k <= 16:
-        return "k_gram_mf_stream + k_gram_combine"
-    # k in {32, 64}: + the list-ordered residuals k_score_mf_mfma reads (k_lres_mf, both sides)
-    return "k_gram_mf_mfma + k_lres_mf"
+    # k in {32, 64}: the Gram pass also writes the list-ordered residuals k_score_mf_mfma reads
+    return "k_gram_mf_stream + k_gram_combine" if k <= 16 else "k_gram_mf_mfma"
 
 
 def side_dim(model, k):
