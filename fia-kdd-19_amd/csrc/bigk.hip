@@ -170,14 +170,18 @@ __global__ void k_self(int64_t N, int64_t n_ent, const int64_t* __restrict__ ptr
   }
 }
 
-// MF residual by train row (user-major pass): e_j = p_u.q_i + b_u + b_i + g - y_j (mf:89-116)
+// MF residual by train row (user-major pass): e_j = p_u.q_i + b_u + b_i + g - y_j (mf:89-116).
+// fia_prepare_for (mark != nullptr): only the rows the shard's scoring reads -- those in a
+// cached user's or a cached item's list (a query (u, i) scores exactly the lists of u and i)
 template <int K>
 __global__ void k_resid_mf(int64_t N, const int32_t* __restrict__ self0, const int32_t* __restrict__ other0,
                            const int32_t* __restrict__ row0, const float* __restrict__ rat0,
                            const float* __restrict__ P, const float* __restrict__ Qt, const float* __restrict__ bu,
-                           const float* __restrict__ bi, const float* __restrict__ gb, double* __restrict__ resid) {
+                           const float* __restrict__ bi, const float* __restrict__ gb, double* __restrict__ resid,
+                           const uint8_t* __restrict__ mark, int64_t U) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (int64_t)gridDim.x * blockDim.x) {
     const int32_t u = self0[p], i = other0[p];
+    if (mark && !mark[u] && !mark[U + i]) continue;
     const float4* a = reinterpret_cast<const float4*>(P + (int64_t)u * K);
     const float4* b = reinterpret_cast<const float4*>(Qt + (int64_t)i * K);
     double acc = 0.0;
@@ -1847,7 +1851,8 @@ hipError_t prepare_big_impl(fia_ctx* c, int64_t Q, const int32_t* qu, const int3
     if (N > 0) {
       hipLaunchKernelGGL(k_resid_mf<K>, dim3(gN), dim3(256), 0, s, N, c->self[0].as<int32_t>(),
                          X.side[0].other.as<int32_t>(), X.side[0].row.as<int32_t>(), X.side[0].rating.as<float>(),
-                         c->p.t[0], c->p.t[1], c->p.t[2], c->p.t[3], c->p.t[4], c->resid.as<double>());
+                         c->p.t[0], c->p.t[1], c->p.t[2], c->p.t[3], c->p.t[4], c->resid.as<double>(),
+                         qu ? c->mark.as<uint8_t>() : nullptr, n_ent[0]);
       FIA_HIP_TRY(hipGetLastError());
     }
   } else {
