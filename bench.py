@@ -65,14 +65,15 @@ FP64_PEAK_TFS = 78.6       # MI355X dense FP64 (vector and matrix; tools/mb_f64.
 # query_cost: a query's fixed work (its solve, chunk lists and share of the Gram pass) in units
 # of one related rating's scoring time, for the strong-scaling split (n_q + query_cost per
 # query); from the round-4 per-phase timings: e.g. 20M MF k=64 61 ns per
-# query over 6.0 ps per scored rating
+# query over 6.0 ps per scored rating; 20M MF k=64 refitted in round 6 from the 8 shards' steps at
+# HEAD (step = 5.83 ps per related rating + 90.7 ns per query, fit residual < 0.1 ms)
 CONFIGS = {
     "ml1m-mf": dict(workload="MF k=16 ml-1m-ex, all 12,074 test ratings (config 2)", model="MF", k=16, data="ml1m",
                     scaling="weak", query_cost=560, inflight=2),
     "yelp-ncf": dict(workload="NCF k=16 yelp-ex, all 51,153 test ratings (config 3)", model="NCF", k=16, data="yelp",
                      scaling="weak", query_cost=210, inflight=2),
     "20m-mf64": dict(workload="MF k=64 synthetic 20M ratings, 276,986 held-out queries (config 4)", model="MF",
-                     k=64, data="20m", scaling="strong", query_cost=10100),
+                     k=64, data="20m", scaling="strong", query_cost=15600),
     "20m-mf256": dict(workload="MF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 257^2 "
                       "blocks per query)", model="MF", k=256, data="20m", scaling="strong", query_cost=150000),
     "20m-ncf256": dict(workload="NCF k=256 synthetic 20M ratings, 276,986 held-out queries (config 5, 2 x 512^2 "
