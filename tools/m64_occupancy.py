@@ -2,8 +2,9 @@
 of k_score_mf_mfma are, and the issue floors that follow (profiles/round5_m64.md).
 
 A work item of k_score_mf_mfma is (<= kMfmaCPI = 4 list chunks of kChunk = 256 ratings of one
-entity) x (<= kMfmaQB = 15 batch queries sharing that entity); per 16-rating tile it runs k/4
-MFMAs whose A rows are the block's queries (+ the entity's own row).  This script rebuilds the
+entity) x (<= kMfmaQB = 16 batch queries sharing that entity; 15 + the entity's own row before
+round 6's Gram-pass residuals); per 16-rating tile it runs k/4 MFMAs whose A rows are the block's
+queries.  This script rebuilds the
 bench's batches (item-major order, --batch-rows 2^29 related ratings) from the same synthetic
 draw and counts, per batch: work items, 16-rating tiles, live query rows per tile, outputs.
 usage: python tools/m64_occupancy.py   (about a minute: the 20M draw)"""
@@ -16,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "fia-kdd-19_amd"))
 from influence import synth  # noqa: E402
 
-QB, CPI, CHUNK, K = 15, 4, 256, 64
+QB, CPI, CHUNK, K = 16, 4, 256, 64
 BATCH_ROWS = 1 << 29
 
 
@@ -59,7 +60,7 @@ def main():
     print("batches %d, queries %d, outputs %.3f G" % (nb, qu.size, tot["outputs"] / 1e9))
     print("per batch: work items %.0f, 16-rating tiles %.0f, MFMAs %.0f" % (tot["items"] / nb, tot["tiles"] / nb,
                                                                           mfma / nb))
-    print("live query rows per 16-row tile: %.2f of 15 (user side %.2f, item side %.2f)" % (
+    print("live query rows per 16-row tile: %.2f of 16 (user side %.2f, item side %.2f)" % (
         tot["live"] / tot["tiles"], tot["live_u"] / max(tot["tiles_u"], 1), tot["live_i"] / max(tot["tiles_i"], 1)))
     print("tiles: user side %.1f %%, item side %.1f %%" % (100 * tot["tiles_u"] / tot["tiles"],
                                                             100 * tot["tiles_i"] / tot["tiles"]))
