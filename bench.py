@@ -643,7 +643,11 @@ def main():
         return j
 
     def exchange(j=0):
-        if tg is not None:
+        if tg is None:
+            return
+        # on the lane's own stream: the pack (and, with RCCL, the collective's enqueue) is
+        # ordered after that lane's kernels, without making the other lane's stream wait
+        with torch.cuda.stream(streams[j]):
             a, b = lanes[j]["tix"][:Q * K].view(Q, K), lanes[j]["tv"][:Q * K].view(Q, K)
             if gdev.type == "cpu":
                 a, b = a.cpu(), b.cpu()
