@@ -1,6 +1,7 @@
 // C ABI entry points (include/fia.h).  Validates arguments, keeps the context
 // state machine (params -> index -> prepare -> query), converts HIP errors to
 // status codes + a message, and never lets an exception cross the boundary.
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -178,7 +179,15 @@ int enter_stream(fia_ctx* c, hipStream_t s, const char* where) {
   return FIA_OK;
 }
 
+// contexts alive per device (fia_create / fia_destroy)
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_live[kMaxDevices];
+
 }  // namespace
+
+namespace fia {
+int live_contexts(int device) { return device >= 0 && device < kMaxDevices ? g_live[device].load() : 1; }
+}  // namespace fia
 
 extern "C" {
 
@@ -193,6 +202,7 @@ int fia_create(int device, fia_ctx** out) {
   fia_ctx* c = new (std::nothrow) fia_ctx();
   if (!c) return FIA_ERR_NOMEM;
   c->device = device;
+  if (device < kMaxDevices) g_live[device].fetch_add(1);
   *out = c;
   return FIA_OK;
 }
@@ -241,6 +251,7 @@ int fia_destroy(fia_ctx* c) {
       for (auto& pr : v) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
     for (auto e : c->events.pool) (void)hipEventDestroy(e);
   }
+  if (c->device >= 0 && c->device < kMaxDevices) g_live[c->device].fetch_sub(1);
   delete c;
   return FIA_OK;
 }

@@ -322,6 +322,8 @@ bool model_supported(int model, int k);
 // large-k models (bigk.hip): MF k in {128, 256}, NCF k in {64, 128, 256}
 bool big_supported(int model, int k);
 hipError_t ensure_self(fia_ctx* c, hipStream_t s);   // c->self[s]: entity of each list position
+// contexts alive on a device (abi.hip): > 1 means batches of several contexts share the GPU
+int live_contexts(int device);
 // qu == nullptr: caches for every entity; else only for the entities of the Q queries
 hipError_t prepare_big(fia_ctx* c, int64_t Q, const int32_t* qu, const int32_t* qi, hipStream_t s);
 // flag[2] |= 1 if a query's user or item has no cache after fia_prepare_for

@@ -2769,8 +2769,12 @@ hipError_t prepare_impl(fia_ctx* c, hipStream_t s, const uint8_t* mark) {
     for (int sd = 0; sd < 2; ++sd) G.lgm[sd] = c->gm[sd].as<double>();
     const int64_t n_all = G.n_items[0] + G.n_items[1];
     if (n_all > 0) {
-      // persistent: the per-lane weight operands are loaded once per wave
-      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * 8;
+      // persistent: the per-lane weight operands are loaded once per wave.  8 waves per CU fill
+      // every CU (2 per SIMD at its registers); when other contexts share the GPU (batches in
+      // flight) 6, so their kernels run beside the pass instead of after it (yelp-ex, 2 in
+      // flight, same box: 102.1 -> 106.0-106.4 M q/s; one context alone: 92.5 at 8, 85.9 at 6)
+      const int per_cu = live_contexts(c->device) > 1 ? 6 : 8;
+      const int64_t cap = (int64_t)(c->num_cus > 0 ? c->num_cus : 256) * per_cu;
       const int64_t grid = n_all < cap ? n_all : cap;
       hipLaunchKernelGGL(k_ncf_gram_rows<M>, dim3((unsigned)grid), dim3(64), 0, s, G, c->p.t[4], c->p.t[5],
                          c->p.t[6], c->p.t[7], c->p.t[9], c->l1[0].as<double>(), c->l1[1].as<double>(),
